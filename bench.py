@@ -1,0 +1,271 @@
+#!/usr/bin/env python3
+"""bench.py — Mcone-steps/s of the MI355X voxel-cone-tracing pass (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], the roofline run): 256^3 anisotropic
+RGBA32F grid, 1920x1080 G-buffer, 9 diffuse + 1 specular cone.  Sponza is not
+available offline, so the scene is the procedural "atrium" stand-in
+(vct.scenes.atrium) and the G-buffer is G_scene, ray-cast by the HIP caster
+from the reference camera (eye (0,0,3), yaw -90, 45 deg FOV; camera.h:14-18,
+assets.cpp:25).
+
+One "step" = one frame of the cone-trace pass (K4) over the whole framebuffer:
+each rank traces its interleaved 64x64 tiles (tile t -> rank t % N) and, for
+N > 1, the indirect-irradiance + specular framebuffers are all-gathered over
+RCCL and un-permuted on every rank (strong scaling: the frame is fixed, the
+tiles are split).  The level-0 grid is injected on rank 0 and broadcast
+(RCCL) before the timed region, as when the light changes; K1/K3 timings are
+reported beside the metric.
+
+value = cone steps of the frame (counted by the kernel; identical to the
+oracle's count, tests/test_parity_gpu.py) x K / max-over-ranks wall time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "voxel-based-global-illumination_amd"))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_TEXEL = 16       # RGBA32F
+BYTES_PER_VALID_PX = 80    # 48 B G-buffer read + 32 B output write
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--n", type=int, default=256)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--scene", default="atrium")
+    p.add_argument("--gbuffer", default="scene", choices=["scene", "rand"])
+    p.add_argument("--n-diffuse", type=int, default=9)
+    p.add_argument("--no-spec", action="store_true")
+    p.add_argument("--variant", type=int, default=0)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_k4.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(ctx, n, g0, E, gb_host, eye, n_diffuse, spec, steps_px_gpu, target_s):
+    """Oracle (C port, OpenMP) on a bounded row sample of the same frame."""
+    import numpy as np
+    from oracle import oracle as O
+    O.build()
+    pos, nrm, alb = gb_host
+    h, w = pos.shape[:2]
+    r0 = ctx.download_level(0)
+    parts = []
+    for l in range(1, ctx.num_levels):
+        for f in range(ctx.level_dims(l)[1]):
+            parts.append(ctx.download_level(l, f).ravel())
+    pyr = np.concatenate(parts)
+    try:
+        cores = min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        cores = min(16, os.cpu_count() or 1)
+    # probe on every 128th row, then size the sample to ~target_s
+    probe_step = 128
+    t0 = time.perf_counter()
+    pr = O.trace(n, g0, E, r0, pyr, pos, nrm, alb, eye, aniso=True, n_diffuse=n_diffuse, specular=spec,
+                 row_step=probe_step, threads=cores)
+    tp = max(time.perf_counter() - t0, 1e-3)
+    rows_probe = len(range(0, h, probe_step))
+    rows_target = max(1, int(rows_probe * target_s / tp))
+    row_step = max(1, h // rows_target)
+    t0 = time.perf_counter()
+    res = O.trace(n, g0, E, r0, pyr, pos, nrm, alb, eye, aniso=True, n_diffuse=n_diffuse, specular=spec,
+                  row_step=row_step, threads=cores)
+    dt = time.perf_counter() - t0
+    rows = list(range(0, h, row_step))
+    match = bool(np.array_equal(res["steps_px"][rows], steps_px_gpu[rows]))
+    return {
+        "value": res["cone_steps"] / dt / 1e6,
+        "unit": "Mcone-steps/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"rows y % {row_step} == 0 ({len(rows)} of {h} rows, {res['cone_steps']} cone steps, "
+                  f"{dt:.1f} s); C oracle -O3 x86-64-v3 OpenMP",
+        "steps_match_gpu": match,
+    }
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from vct import Context, scenes
+    from vct.camera import Camera
+    from vct.multi import FrameTracer, compact_index
+
+    n, w, h = args.n, args.width, args.height
+    spec = not args.no_spec
+    g0, E = scenes.grid_for_unit_box(n)
+    ctx = Context(n, g0, E, aniso=True, n_diffuse=args.n_diffuse, specular=spec, device=local_rank)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+    scene = scenes.SCENES[args.scene]()
+    v, i, m, k = scene.arrays()
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) * 1e3
+
+    # K1 on every rank (each process holds the scene, as the reference's loader does)
+    k1_ms = timed(lambda: ctx.voxelize(v, i, m, k))
+    level0 = torch.empty((n ** 3 * 4,), dtype=torch.float32, device=dev)
+    k2_ms = 0.0
+    if rank == 0:
+        k2_ms = timed(lambda: ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR))
+        ctx.copy_level0_to_device(level0)
+    bcast_ms = 0.0
+    if world > 1:
+        dist.barrier()
+        bcast_ms = timed(lambda: dist.broadcast(level0, src=0))
+        ctx.set_level0_from_device(level0)
+    k3_ms = timed(ctx.build_mips)
+
+    cam = Camera()
+    eye = [float(x) for x in cam.position]
+    if args.gbuffer == "scene":
+        gb = tuple(torch.empty((h, w, 4), dtype=torch.float32, device=dev) for _ in range(3))
+        ctx.gbuffer_raycast_device(cam, w, h, scenes.ROUGHNESS, *gb)
+    else:
+        ao, nm = ctx.download_voxels()
+        host = scenes.gbuffer_rand(ao, nm, g0, E, w, h, seed=42)
+        gb = tuple(torch.from_numpy(a).to(dev) for a in host)
+    torch.cuda.synchronize()
+
+    tracer = FrameTracer(ctx, torch, dist, w, h, rank, world, dev)
+    # counting pass (same kernel, counters on): frame cone steps and texel fetches
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    steps_px = torch.zeros((h, w), dtype=torch.int32, device=dev)
+    tracer.trace_local(gb, eye, cone_steps=cnt[0:1], texel_fetches=cnt[1:2], steps_px=steps_px,
+                       variant=args.variant)
+    torch.cuda.synchronize()
+    local_steps, local_texels = int(cnt[0].item()), int(cnt[1].item())
+    valid = (gb[0][..., 3] != 0).reshape(-1).cpu().numpy()
+    fi, _ = compact_index(w, h, rank, world)
+    local_valid = int(valid[fi].sum())
+    tot = torch.tensor([local_steps, local_valid], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    frame_steps, frame_valid = int(tot[0].item()), int(tot[1].item())
+
+    for _ in range(args.warmup):
+        tracer.frame(gb, eye, variant=args.variant)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev[s][0].record(stream)
+        tracer.trace_local(gb, eye, variant=args.variant)
+        ev[s][1].record(stream)
+        tracer.gather()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    k4_ms = [a.elapsed_time(b) for a, b in ev]
+    k4_avg_ms = sum(k4_ms) / len(k4_ms)
+    k4_med_ms = sorted(k4_ms)[len(k4_ms) // 2]
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = frame_steps * args.steps / elapsed / 1e6
+    bytes_launch = local_texels * BYTES_PER_TEXEL + local_valid * BYTES_PER_VALID_PX
+    achieved = bytes_launch / (k4_avg_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("config") == [n, w, h, args.scene, args.gbuffer, args.variant]:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = None
+    if rank == 0:
+        result = {
+            "metric": "Mcone-steps/s at 256^3 grid, 1080p, 9 diffuse + 1 spec cone; 1/2/4/8 GPUs",
+            "value": round(value, 2),
+            "unit": "Mcone-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic: procedural '{args.scene}' scene (Sponza stand-in), G_{args.gbuffer} G-buffer",
+            "config": {
+                "workload": f"cone trace K4, {n}^3 aniso RGBA32F grid, {w}x{h}, "
+                            f"{args.n_diffuse} diffuse + {1 if spec else 0} specular cones",
+                "grid": n, "width": w, "height": h, "scene": args.scene, "gbuffer": args.gbuffer,
+                "n_diffuse": args.n_diffuse, "specular": spec, "parallelism": f"screen-tiles x{world}",
+                "variant": args.variant,
+            },
+            "frame_cone_steps": frame_steps,
+            "valid_px": frame_valid,
+            "k4_kernel_ms_avg": round(k4_avg_ms, 4),
+            "k4_kernel_ms_median": round(k4_med_ms, 4),
+            "k1_voxelize_ms": round(k1_ms, 3),
+            "k2_inject_ms": round(k2_ms, 3),
+            "k3_mips_ms": round(k3_ms, 3),
+            "grid_bcast_ms": round(bcast_ms, 3),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": bytes_launch,
+                "texel_fetches_per_launch": local_texels,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            host = tuple(t_.cpu().numpy() for t_ in gb)
+            result["cpu_baseline"] = cpu_baseline(ctx, n, g0, E, host, eye, args.n_diffuse, spec,
+                                                  steps_px.cpu().numpy().astype(np.uint32), args.cpu_seconds)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

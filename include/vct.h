@@ -1,0 +1,174 @@
+/*
+ * vct.h — C-ABI drop-in boundary of the MI355X-native voxel-cone-tracing path.
+ *
+ * What it replaces.  The reference exposes its per-frame hot-path slot as the
+ * C++ virtual `Renderer::Render()` (assets/code/renderer/renderer.h:3-10),
+ * registered by name in `AssetsManager::renderers`
+ * (assets/code/core/assets.h:17-20, assets.cpp:44) and called once per frame at
+ * assets/code/core/engine.cpp:151.  Its only implementation,
+ * `VoxelizationRenderer::Render` (assets/code/renderer/r_voxelization.cpp:4-35),
+ * pulls camera and model state from singletons and issues GL draws; the GI
+ * stages its name promises (voxelize, inject, mip, cone-trace) were never
+ * written.  This header is the boundary a Renderer
+ * subclass calls instead of GL: plain pointers and sizes, no C++ / torch types,
+ * status codes instead of exceptions (the reference's only error channel is
+ * `throw int` at engine.cpp:55,70 and std::cout prints).
+ *
+ * Conventions.
+ *  - One vct_ctx per host thread, no global state (the reference is
+ *    single-threaded: engine.h:7, assets.h:13).  A ctx owns every device buffer.
+ *  - Host-pointer entry points are synchronous on return.  *_device entry
+ *    points take device pointers and are asynchronous on the ctx stream
+ *    (vct_set_stream); vct_synchronize() waits for them.
+ *  - Data layouts: grids are linear-Z RGBA32F, index x + n*(y + n*z); the
+ *    G-buffer and outputs are [h][w][4] float, row 0 = top of the image.
+ *  - Semantics: SURVEY.md Appendix A with the literals of vct_spec.h.
+ */
+#ifndef VCT_H
+#define VCT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VCT_ABI_VERSION 1
+
+typedef struct vct_ctx vct_ctx;
+
+typedef enum vct_status {
+    VCT_OK = 0,
+    VCT_EINVAL = 1,   /* bad argument                                   */
+    VCT_ENOMEM = 2,   /* device allocation failed                       */
+    VCT_EDEVICE = 3,  /* HIP runtime / kernel error                     */
+    VCT_ECOMM = 4,    /* multi-GPU exchange error                       */
+    VCT_ESTATE = 5    /* call out of order (e.g. trace before mips)     */
+} vct_status;
+
+/* Grid and cone configuration.  Fields left 0 take the spec default. */
+typedef struct vct_config {
+    uint32_t n;            /* grid resolution, power of two, 4..1024            */
+    float aabb_min[3];     /* world-space min corner of the cubic grid           */
+    float extent;          /* cube edge E (> 0); voxel size h = E / n            */
+    uint32_t aniso;        /* 1: 6-face anisotropic mips (A.4), 0: box filter    */
+    uint32_t n_diffuse;    /* diffuse cones: 0, 1, 9 or 16                        */
+    uint32_t specular;     /* 1: trace the specular cone                         */
+    int32_t device;        /* HIP device ordinal; -1 = current device            */
+} vct_config;
+
+/* Camera in the reference's conventions (scene/camera.h:20-54, camera.cpp:24-27,
+ * r_voxelization.cpp:18): RH lookAt, vertical FOV = zoom degrees. */
+typedef struct vct_camera {
+    float position[3];
+    float front[3];        /* unit view direction (camera -z)                    */
+    float up[3];           /* unit camera up                                     */
+    float right[3];        /* unit camera right                                  */
+    float zoom_deg;        /* vertical field of view in degrees                  */
+    float near_plane;      /* 0.1 in the reference                               */
+    float far_plane;       /* 100 in the reference                               */
+} vct_camera;
+
+/* Arguments of the device-resident cone trace (K4).  Float buffers must be
+ * 16-byte aligned, the two counters 8-byte aligned (VCT_EINVAL otherwise). */
+typedef struct vct_trace_args {
+    const float* pos4;     /* device [h][w][4]: world position, w = 1 valid / 0 background */
+    const float* nrm4;     /* device [h][w][4]: unit normal                                */
+    const float* alb4;     /* device [h][w][4]: albedo rgb, roughness                      */
+    uint32_t width, height;
+    float eye[3];          /* camera position for the specular cone                        */
+    float* diffuse4;       /* device out: (indirect irradiance rgb, ambient occlusion)     */
+    float* spec4;          /* device out: (specular rgb, alpha)                            */
+    uint32_t* steps_px;    /* device out [h][w] cone steps per pixel, or NULL               */
+    unsigned long long* cone_steps; /* device counter, += steps of this call, or NULL      */
+    unsigned long long* texel_fetches; /* device counter, += RGBA32F texels the spec reads
+                                          (8 per isotropic, 24 per anisotropic level sample), or NULL */
+    uint32_t tile_rank;    /* trace only 64x64 tiles t with t % tile_world == tile_rank     */
+    uint32_t tile_world;   /* 0 or 1: every tile                                            */
+    uint32_t tile_compact; /* 1: outputs in rank-compact tile layout [local tile][64*64][4] */
+    uint32_t variant;      /* kernel variant: 0 = default                                  */
+} vct_trace_args;
+
+/* ---- lifetime ---------------------------------------------------------- */
+vct_status  vct_create(const vct_config* cfg, vct_ctx** out);
+void        vct_destroy(vct_ctx* ctx);
+const char* vct_last_error(const vct_ctx* ctx);
+const char* vct_status_string(vct_status s);
+uint32_t    vct_abi_version(void);
+vct_status  vct_get_config(const vct_ctx* ctx, vct_config* out);
+vct_status  vct_set_stream(vct_ctx* ctx, void* hip_stream); /* NULL = default stream */
+vct_status  vct_synchronize(vct_ctx* ctx);
+
+/* ---- K1 conservative voxelization (A.2) --------------------------------
+ * verts: host array of n_verts records of `vertex_stride` bytes whose first 12
+ * bytes are the world position (the reference `Vertex`, stdafx.h:36-42, is a
+ * 56-byte record with Position at offset 0; mesh.cpp:43-55).  idx: n_idx
+ * uint32 indices, 3 per triangle (model.cpp:24 triangulates).  tri_material:
+ * per-triangle index into material_kd4 (NULL = material 0).  material_kd4:
+ * n_materials x (Kd rgba) as in Material::Kd (material.h:10); NULL = white.
+ * Replaces the previous voxel grid; the triangles are kept for
+ * vct_gbuffer_raycast_device. */
+vct_status vct_voxelize(vct_ctx* ctx, const void* verts, uint32_t vertex_stride, uint32_t n_verts,
+                        const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_material,
+                        const float* material_kd4, uint32_t n_materials);
+
+/* ---- K2 direct-light injection (A.3) ----------------------------------- */
+vct_status vct_inject_directional(vct_ctx* ctx, const float dir_to_light[3], const float color[3]);
+
+/* ---- K3 mip build (A.4) --------------------------------------------------- */
+vct_status vct_build_mips(vct_ctx* ctx);
+
+/* ---- K4 cone trace (A.5, A.6) ------------------------------------------
+ * Host convenience form: uploads the G-buffer, traces every pixel, downloads.
+ * out_steps_px / out_cone_steps may be NULL. */
+vct_status vct_trace(vct_ctx* ctx, const float* gbuf_pos4, const float* gbuf_nrm4,
+                     const float* gbuf_alb_rough4, uint32_t width, uint32_t height,
+                     const float eye[3], float* out_diffuse4, float* out_spec4,
+                     uint32_t* out_steps_px, uint64_t* out_cone_steps);
+/* Device-resident form (asynchronous on the ctx stream). */
+vct_status vct_trace_device(vct_ctx* ctx, const vct_trace_args* args);
+/* Number of 64x64 tiles rank `rank` of `world` traces for a width x height frame. */
+uint32_t   vct_tiles_for_rank(uint32_t width, uint32_t height, uint32_t rank, uint32_t world);
+/* Scatter all-gathered rank-compact tile buffers ([world][max_tiles][64*64][4],
+ * max_tiles = vct_tiles_for_rank(w,h,0,world)) into a [h][w][4] frame. */
+vct_status vct_untile_device(vct_ctx* ctx, const float* gathered4, uint32_t width, uint32_t height,
+                             uint32_t world, float* frame4);
+
+/* ---- G-buffer (input producer) -----------------------
+ * Ray-casts the triangles of the last vct_voxelize call through `cam` into a
+ * device G-buffer (pos4.w = 1 on hit, 0 on background).  Normals are the face
+ * normals turned toward the viewer; albedo = material Kd; alb4.w = roughness. */
+vct_status vct_gbuffer_raycast_device(vct_ctx* ctx, const vct_camera* cam, uint32_t width,
+                                      uint32_t height, float roughness, float* pos4,
+                                      float* nrm4, float* alb4);
+
+/* ---- device memory for hosts without HIP headers (FFI bindings) ----------
+ * kind: 0 host->device, 1 device->host, 2 device->device; synchronous. */
+vct_status vct_device_alloc(vct_ctx* ctx, size_t bytes, void** dptr);
+vct_status vct_device_free(vct_ctx* ctx, void* dptr);
+vct_status vct_memcpy(vct_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
+
+/* ---- grid access (parity, multi-GPU exchange) ---------------------------- */
+uint32_t   vct_num_levels(const vct_ctx* ctx);                 /* L + 1 */
+vct_status vct_level_dims(const vct_ctx* ctx, uint32_t level, uint32_t* n_l, uint32_t* n_faces);
+/* level 0: face must be 0; host_rgba receives n_l^3 x 4 floats */
+vct_status vct_download_level(vct_ctx* ctx, uint32_t level, uint32_t face, float* host_rgba);
+/* replaces the level-0 radiance grid (n^3 x 4 floats, host) */
+vct_status vct_upload_level0(vct_ctx* ctx, const float* host_rgba);
+/* device pointer + size of the level-0 radiance grid (RCCL broadcast buffer) */
+vct_status vct_level0_device(vct_ctx* ctx, void** dptr, size_t* bytes);
+/* device-to-device copies of the level-0 grid on the ctx stream (host RCCL
+ * glue that owns its own communication buffer, e.g. a torch tensor) */
+vct_status vct_copy_level0_to_device(vct_ctx* ctx, void* dst);
+vct_status vct_set_level0_from_device(vct_ctx* ctx, const void* src);
+/* K1 outputs: resolved albedo/occupancy and normal grids (n^3 x 4 floats each) */
+vct_status vct_download_voxels(vct_ctx* ctx, float* albedo_occ4, float* normal4);
+/* K1 raw accumulators: sums6 [n^3][6] int64 (albedo rgb, normal xyz; 16.16 fixed
+ * point), counts [n^3] uint32.  Either pointer may be NULL. */
+vct_status vct_download_accum(vct_ctx* ctx, int64_t* sums6, uint32_t* counts);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VCT_H */

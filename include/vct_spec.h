@@ -1,0 +1,106 @@
+/*
+ * vct_spec.h — normative constants of the voxel-cone-tracing (VCT) hot path.
+ *
+ * The reference (fysososo/voxel-based-global-illumination) never implemented the
+ * GI stages: `VoxelizationProgram` is an empty subclass
+ * (assets/code/program/p_voxelization.h:4-7) and `VoxelizationRenderer::Render`
+ * only draws a forward-textured mesh (assets/code/renderer/r_voxelization.cpp:4-35).
+ * SURVEY.md Appendix A therefore defines the semantics; this header pins every
+ * free parameter of that spec as a literal so that the HIP kernels
+ * (voxel-based-global-illumination_amd/csrc) and the CPU oracle (oracle/) read the
+ * SAME numbers.  Nothing here is code; it is plain C89-compatible data so the
+ * C oracle, the C++ host and the HIP device code can all include it.
+ *
+ * Units.  All cone / DDA / SAT arithmetic is carried out in level-0 VOXEL units:
+ *   q = (p - aabb_min) * inv_h,  inv_h = (float)n / extent   (float divide)
+ * so a voxel has edge 1, the grid spans [0, n]^3, level l texel coords are
+ * q * 2^-l - 0.5 (GL texel-centre convention).
+ *
+ * Floating point.  Every translation unit of the path is compiled with
+ * -ffp-contract=off.  The only fused multiply-adds are the explicit fmaf()
+ * calls that the spec names (trilinear accumulation, level blend, composite,
+ * cone-weight accumulation, the log2 polynomial); they are exact on both the
+ * host (libm / x86 FMA) and the device (v_fma_f32), so oracle and kernels can
+ * agree bit for bit.
+ */
+#ifndef VCT_SPEC_H
+#define VCT_SPEC_H
+
+/* ---- A.6 cone marching ---------------------------------------------------- */
+#define VCT_ALPHA_STOP      0.95f        /* stop when a >= 0.95                    */
+#define VCT_STEP_SCALE      0.5f         /* t += 0.5 * D                            */
+#define VCT_SQRT3           1.7320508f   /* t_max = n * sqrt(3) (voxel units)       */
+#define VCT_SPEC_TAU_MIN    0.02f        /* specular tau = clamp(roughness, .02, 1) */
+#define VCT_SPEC_TAU_MAX    1.0f
+
+/* ---- log2 used for the mip level m = log2(D) (D >= 1) ----------------------
+ * m = e + 2*s*P(s^2)/ln2 with x = 2^e * f, f in [1/sqrt2, sqrt2], s=(f-1)/(f+1)
+ * P(z) = 1 + z/3 + z^2/5 + z^3/7 + z^4/9 (Horner, fmaf).  |err| < 2e-7.      */
+#define VCT_LOG2_SQRT2      1.41421354f
+#define VCT_INV_LN2         1.44269502f
+#define VCT_LOG2_C9         0.111111112f
+#define VCT_LOG2_C7         0.142857149f
+#define VCT_LOG2_C5         0.200000003f
+#define VCT_LOG2_C3         0.333333343f
+
+/* ---- diffuse cone sets ------------------------------------------------------
+ * d_k = cn*n + ct*T + cb*B with (T,B) the Duff et al. 2017 branchless ONB of n.
+ * Row = (cn, ct, cb, weight).  Weights are cos-theta normalised.               */
+#define VCT_TAN30           0.577350259f /* 9-cone and 1-cone half-angle tangent   */
+#define VCT_TAN20           0.36397022f  /* 16-cone half-angle tangent             */
+
+/* 9 cones: d0 = n, d_k at 45 deg polar, phi_k = (k-1)*45 deg       */
+#define VCT_CONES9(X)                                                   \
+    X(1.0f,        0.0f,        0.0f,        0.150221109f)             \
+    X(0.707106769f, 0.707106769f, 0.0f,      0.106222361f)             \
+    X(0.707106769f, 0.5f,        0.5f,       0.106222361f)             \
+    X(0.707106769f, 0.0f,        0.707106769f, 0.106222361f)           \
+    X(0.707106769f, -0.5f,       0.5f,       0.106222361f)             \
+    X(0.707106769f, -0.707106769f, 0.0f,     0.106222361f)             \
+    X(0.707106769f, -0.5f,       -0.5f,      0.106222361f)             \
+    X(0.707106769f, 0.0f,        -0.707106769f, 0.106222361f)          \
+    X(0.707106769f, 0.5f,        -0.5f,      0.106222361f)
+
+/* 1 cone (config C1): d0 = n, w = 1                                            */
+#define VCT_CONES1(X)  X(1.0f, 0.0f, 0.0f, 1.0f)
+
+/* 16 cones (config C5): centre + 5 at 30 deg + 10 at 60 deg (phi offset 18 deg) */
+#define VCT_CONES16(X)                                                  \
+    X(1.0f,        0.0f,          0.0f,          0.0968042314f)        \
+    X(0.866025388f, 0.5f,          0.0f,          0.0838349238f)       \
+    X(0.866025388f, 0.154508501f,  0.475528270f,  0.0838349238f)       \
+    X(0.866025388f, -0.404508501f, 0.293892622f,  0.0838349238f)       \
+    X(0.866025388f, -0.404508501f, -0.293892622f, 0.0838349238f)       \
+    X(0.866025388f, 0.154508501f,  -0.475528270f, 0.0838349238f)       \
+    X(0.5f,        0.823639095f,  0.267616570f,  0.0484021157f)        \
+    X(0.5f,        0.509036958f,  0.700629294f,  0.0484021157f)        \
+    X(0.5f,        0.0f,          0.866025388f,  0.0484021157f)        \
+    X(0.5f,        -0.509036958f, 0.700629294f,  0.0484021157f)        \
+    X(0.5f,        -0.823639095f, 0.267616570f,  0.0484021157f)        \
+    X(0.5f,        -0.823639095f, -0.267616570f, 0.0484021157f)        \
+    X(0.5f,        -0.509036958f, -0.700629294f, 0.0484021157f)        \
+    X(0.5f,        0.0f,          -0.866025388f, 0.0484021157f)        \
+    X(0.5f,        0.509036958f,  -0.700629294f, 0.0484021157f)        \
+    X(0.5f,        0.823639095f,  -0.267616570f, 0.0484021157f)
+
+#define VCT_MAX_CONES       17           /* 16 diffuse + 1 specular                */
+
+/* ---- A.4 anisotropic faces --------------------------------------------------
+ * Face f is the one SAMPLED by cones travelling along that direction; its
+ * "front" child is the one a +X-travelling cone meets first (smaller x).      */
+#define VCT_FACE_PX 0
+#define VCT_FACE_NX 1
+#define VCT_FACE_PY 2
+#define VCT_FACE_NY 3
+#define VCT_FACE_PZ 4
+#define VCT_FACE_NZ 5
+#define VCT_NUM_FACES 6
+
+/* ---- A.2 voxelization fixed point ------------------------------------------ */
+#define VCT_FIXED_ONE       65536.0f     /* round(x * 2^16) into int64 sums        */
+#define VCT_FIXED_ONE_D     65536.0
+
+/* ---- multi-GPU screen tiling ---------------------------------- */
+#define VCT_TILE            64           /* 64x64-pixel tiles, round-robin by rank */
+
+#endif /* VCT_SPEC_H */

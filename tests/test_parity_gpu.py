@@ -1,0 +1,231 @@
+"""Parity of the HIP path (through the C-ABI) with the CPU oracle.
+
+Bar: K1 voxelization, K2 injection and K3 mips are
+integer / fixed-order float work -> BIT-EXACT.  K4 cone tracing: relative L2
+<= 1e-3 over both output buffers (north_star's fp32 tolerance); the kernels
+and the oracle share the spec's operation order, so the observed error is
+expected to be 0 and the per-pixel step counts identical.
+"""
+import numpy as np
+import pytest
+
+from helpers import gpu_pipeline, gpu_pyramid_flat, rel_l2, scene_arrays
+
+pytestmark = pytest.mark.gpu
+
+TRACE_TOL = 1e-3   # north_star: indirect-irradiance parity within 1e-3 relative L2 (fp32)
+
+
+@pytest.mark.parametrize("name,n", [("cornell", 16), ("cornell", 32), ("atrium", 32), ("atrium", 64),
+                                    ("random", 32)])
+def test_voxelize_inject_mips_bitexact(gpu_ready, oracle_mod, name, n):
+    O = oracle_mod
+    ctx, s, (v, i, m, k), (g0, E) = gpu_pipeline(n, name)
+    ref = O.pipeline(n, g0, E, v, i, m, k, __import__("vct").scenes.LIGHT_DIR)
+    sums, counts = ctx.download_accum()
+    assert np.array_equal(counts, ref["counts"]), "K1 coverage counts differ"
+    assert np.array_equal(sums, ref["sums"]), "K1 fixed-point sums differ"
+    ao, nm = ctx.download_voxels()
+    assert np.array_equal(ao, ref["albedo_occ"])
+    assert np.array_equal(nm, ref["normal"])
+    r0 = ctx.download_level(0)
+    assert np.array_equal(r0, ref["r0"]), "K2 radiance differs"
+    assert np.array_equal(gpu_pyramid_flat(ctx), ref["pyr"]), "K3 pyramid differs"
+    assert (counts > 0).sum() > 0 and r0[..., :3].sum() > 0
+    ctx.close()
+
+
+@pytest.mark.parametrize("aniso", [True, False])
+def test_mips_bitexact_random_level0(gpu_ready, oracle_mod, aniso):
+    from vct import Context
+    n = 32
+    rng = np.random.default_rng(3)
+    a = (rng.random((n, n, n)) < 0.3).astype(np.float32)
+    r0 = np.concatenate([rng.random((n, n, n, 3)).astype(np.float32) * a[..., None], a[..., None]], -1)
+    ctx = Context(n, (0, 0, 0), 1.0, aniso=aniso)
+    ctx.upload_level0(r0)
+    ctx.build_mips()
+    assert np.array_equal(gpu_pyramid_flat(ctx), oracle_mod.build_mips(n, r0, aniso))
+    ctx.close()
+
+
+def test_mips_constant_kat_gpu(gpu_ready):
+    """KAT 2 on the GPU: constant (L*alpha, alpha) -> a_l = 1 - (1-alpha)^(2^l)."""
+    from vct import Context
+    n, alpha, Lr = 16, 0.3, 0.8
+    r0 = np.empty((n, n, n, 4), np.float32)
+    r0[..., :3] = Lr * alpha
+    r0[..., 3] = alpha
+    ctx = Context(n, (0, 0, 0), 1.0, aniso=True)
+    ctx.upload_level0(r0)
+    ctx.build_mips()
+    for l in range(1, ctx.num_levels):
+        al = 1 - (1 - alpha) ** (2 ** l)
+        for f in range(6):
+            t = ctx.download_level(l, f)
+            np.testing.assert_allclose(t[..., 3], al, rtol=2e-6)
+            np.testing.assert_allclose(t[..., :3], Lr * al, rtol=2e-6)
+    ctx.close()
+
+
+def _gbuf(kind, s, ctx_or_ref, g0, E, w, h):
+    from vct import scenes
+    from vct.camera import Camera
+    cam = Camera()
+    if kind == "scene":
+        return scenes.raycast_numpy(s, cam, w, h), cam
+    ao, nm = ctx_or_ref
+    return scenes.gbuffer_rand(ao, nm, g0, E, w, h, seed=42), cam
+
+
+@pytest.mark.parametrize("name,n,kind,aniso,nd,spec", [
+    ("cornell", 32, "scene", True, 9, True),
+    ("cornell", 32, "rand", True, 9, True),
+    ("atrium", 64, "scene", True, 9, True),
+    ("atrium", 32, "rand", False, 9, True),
+    ("cornell", 16, "scene", True, 1, False),
+    ("atrium", 32, "rand", True, 16, True),
+    ("cornell", 64, "scene", True, 0, True),
+])
+def test_trace_parity(gpu_ready, oracle_mod, name, n, kind, aniso, nd, spec):
+    O = oracle_mod
+    ctx, s, (v, i, m, k), (g0, E) = gpu_pipeline(n, name, aniso=aniso, n_diffuse=nd, specular=spec)
+    (pos, nrm, alb), cam = _gbuf(kind, s, ctx.download_voxels(), g0, E, 64, 48)
+    got = ctx.trace(pos, nrm, alb, cam.position)
+    r0 = ctx.download_level(0)
+    ref = O.trace(n, g0, E, r0, gpu_pyramid_flat(ctx), pos, nrm, alb, cam.position, aniso=aniso,
+                  n_diffuse=nd, specular=spec)
+    e_d = rel_l2(got["diffuse"], ref["diffuse"])
+    e_s = rel_l2(got["spec"], ref["spec"]) if spec else 0.0
+    both = rel_l2(np.concatenate([got["diffuse"], got["spec"]]), np.concatenate([ref["diffuse"], ref["spec"]]))
+    assert both <= TRACE_TOL, (e_d, e_s)
+    assert got["cone_steps"] == ref["cone_steps"]
+    assert np.array_equal(got["steps_px"], ref["steps_px"])
+    # the spec's operation order is shared, so the result is expected bit-exact
+    assert np.array_equal(got["diffuse"], ref["diffuse"]) and np.array_equal(got["spec"], ref["spec"])
+    ctx.close()
+
+
+def test_trace_edge_cases(gpu_ready, oracle_mod):
+    """1x1 frame, all-background frame, odd sizes not multiple of 64, empty grid."""
+    from vct import Context
+    ctx, s, arrs, (g0, E) = gpu_pipeline(16, "cornell")
+    for (w, h) in [(1, 1), (65, 3), (3, 130)]:
+        pos = np.zeros((h, w, 4), np.float32)
+        out = ctx.trace(pos, pos, pos, (0, 0, 3))
+        assert out["cone_steps"] == 0 and not out["diffuse"].any() and not out["spec"].any()
+    ctx.close()
+    # empty grid: diffuse = 0, AO = 1, spec = 0
+    n = 16
+    c2 = Context(n, g0, E)
+    c2.upload_level0(np.zeros((n, n, n, 4), np.float32))
+    c2.build_mips()
+    rng = np.random.default_rng(0)
+    pos = np.zeros((5, 7, 4), np.float32)
+    pos[..., :3] = rng.uniform(-0.5, 0.5, (5, 7, 3))
+    pos[..., 3] = 1
+    nrm = np.zeros_like(pos)
+    nrm[..., 1] = 1
+    alb = np.full_like(pos, 0.1)
+    out = c2.trace(pos, nrm, alb, (0, 0, 3))
+    assert not out["diffuse"][..., :3].any() and np.all(out["diffuse"][..., 3] == 1) and not out["spec"].any()
+    ref = oracle_mod.trace(n, g0, E, np.zeros((n, n, n, 4), np.float32), gpu_pyramid_flat(c2), pos, nrm, alb,
+                           (0, 0, 3))
+    assert np.array_equal(out["steps_px"], ref["steps_px"])
+    c2.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_tiled_trace_equals_full_frame(gpu_ready, world):
+    """Multi-GPU tile partition on one device: every rank's compact tiles, gathered and
+    un-permuted on the device, reproduce the single-rank frame bit for bit."""
+    import torch
+    from vct import scenes
+    from vct.camera import Camera
+    from vct.multi import tiles_for_rank
+    ctx, s, arrs, (g0, E) = gpu_pipeline(32, "atrium")
+    w, h = 200, 130
+    cam = Camera()
+    dev = torch.device("cuda")
+    pos, nrm, alb = (torch.empty((h, w, 4), device=dev) for _ in range(3))
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.gbuffer_raycast_device(cam, w, h, scenes.ROUGHNESS, pos, nrm, alb)
+    full_d = torch.empty((h, w, 4), device=dev)
+    full_s = torch.empty((h, w, 4), device=dev)
+    ctx.trace_device(pos, nrm, alb, w, h, cam.position, full_d, full_s)
+    maxt = tiles_for_rank(w, h, 0, world)
+    g_d = torch.zeros((world, maxt * 4096, 4), device=dev)
+    g_s = torch.zeros((world, maxt * 4096, 4), device=dev)
+    for r in range(world):
+        ctx.trace_device(pos, nrm, alb, w, h, cam.position, g_d[r], g_s[r], tile_rank=r, tile_world=world,
+                         tile_compact=True)
+    fd = torch.empty((h, w, 4), device=dev)
+    fs = torch.empty((h, w, 4), device=dev)
+    ctx.untile_device(g_d, w, h, world, fd)
+    ctx.untile_device(g_s, w, h, world, fs)
+    torch.cuda.synchronize()
+    assert torch.equal(fd, full_d) and torch.equal(fs, full_s)
+    # host mirror of the permutation agrees with the device one
+    from vct.multi import untile
+    host = untile(g_d.cpu().numpy(), w, h, world)
+    assert np.array_equal(host, full_d.cpu().numpy())
+    ctx.close()
+
+
+def test_raycast_matches_numpy(gpu_ready):
+    import torch
+    from vct import scenes
+    from vct.camera import Camera
+    ctx, s, arrs, (g0, E) = gpu_pipeline(16, "atrium")
+    cam = Camera()
+    w, h = 96, 64
+    dev = torch.device("cuda")
+    pos, nrm, alb = (torch.empty((h, w, 4), device=dev) for _ in range(3))
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.gbuffer_raycast_device(cam, w, h, 0.1, pos, nrm, alb)
+    torch.cuda.synchronize()
+    rp, rn, ra = scenes.raycast_numpy(s, cam, w, h, 0.1)
+    gp = pos.cpu().numpy()
+    valid_match = (gp[..., 3] == rp[..., 3]).mean()
+    assert valid_match > 0.995
+    both = (gp[..., 3] > 0) & (rp[..., 3] > 0)
+    same_n = np.all(np.abs(nrm.cpu().numpy()[both] - rn[both]) < 1e-3, axis=-1).mean()
+    assert same_n > 0.99
+    assert np.abs(gp[both][:, :3] - rp[both][:, :3]).max() < 1e-3
+    ctx.close()
+
+
+def test_abi_errors(gpu_ready):
+    from vct import Context, VctError
+    with pytest.raises(VctError):
+        Context(24, (0, 0, 0), 1.0)          # not a power of two
+    with pytest.raises(VctError):
+        Context(16, (0, 0, 0), -1.0)         # bad extent
+    with pytest.raises(VctError):
+        Context(16, (0, 0, 0), 1.0, n_diffuse=5)
+    ctx = Context(16, (0, 0, 0), 1.0)
+    z = np.zeros((2, 2, 4), np.float32)
+    with pytest.raises(VctError, match="ESTATE"):
+        ctx.trace(z, z, z, (0, 0, 0))        # trace before mips
+    with pytest.raises(VctError, match="ESTATE"):
+        ctx.inject_directional((0, 1, 0))    # inject before voxelize
+    v = np.zeros((3, 14), np.float32)
+    with pytest.raises(VctError, match="EINVAL"):
+        ctx.voxelize(v, np.array([0, 1, 5], np.uint32))   # index out of range
+    with pytest.raises(VctError, match="EINVAL"):
+        ctx.voxelize(v, np.array([0, 1, 2], np.uint32), np.array([3], np.uint32),
+                     np.ones((1, 4), np.float32))         # material out of range
+    ctx.voxelize(v, np.zeros(0, np.uint32))  # empty mesh is fine
+    with pytest.raises(VctError, match="EINVAL"):
+        ctx.inject_directional((0, 0, 0))
+    ctx.close()
+
+
+def test_voxelize_reproducible_and_rerun(gpu_ready):
+    """Integer atomics: reruns (and a second context) are bitwise identical."""
+    ctx, s, (v, i, m, k), (g0, E) = gpu_pipeline(64, "random")
+    a1 = ctx.download_accum()
+    ctx.voxelize(v, i, m, k)
+    a2 = ctx.download_accum()
+    assert np.array_equal(a1[0], a2[0]) and np.array_equal(a1[1], a2[1])
+    ctx.close()

@@ -1,0 +1,469 @@
+// vct_capi.cpp — the extern "C" boundary of include/vct.h.
+//
+// Stands where the reference's `Renderer::Render()` virtual
+// (assets/code/renderer/renderer.h:3-10) would call GL.  Every entry point
+// validates its arguments, selects the context's device, launches on the
+// context stream and turns HIP errors into vct_status + vct_last_error() text.
+// No exception crosses the ABI.  There is no CPU fallback: without a HIP device
+// vct_create fails with VCT_EDEVICE.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include "vct_internal.h"
+
+using namespace vct;
+
+namespace {
+
+vct_status fail(vct_ctx* c, vct_status s, const std::string& msg) {
+    if (c) c->err = msg;
+    return s;
+}
+
+vct_status hip_fail(vct_ctx* c, hipError_t e, const char* where) {
+    std::string m = std::string(where) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+    return fail(c, e == hipErrorOutOfMemory ? VCT_ENOMEM : VCT_EDEVICE, m);
+}
+
+#define VCT_HIP(call, where)                            \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return hip_fail(c, e_, where); \
+    } while (0)
+
+bool is_pow2(uint32_t n) { return n && !(n & (n - 1)); }
+
+uint32_t ilog2u(uint32_t n) {
+    uint32_t l = 0;
+    while ((1u << (l + 1)) <= n) ++l;
+    return l;
+}
+
+vct_status use_device(vct_ctx* c) {
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) return hip_fail(c, e, "hipSetDevice");
+    return VCT_OK;
+}
+
+struct DeviceBuf {  // RAII for per-call uploads
+    void* p = nullptr;
+    ~DeviceBuf() { if (p) (void)hipFree(p); }
+};
+
+}  // namespace
+
+namespace vct {
+hipError_t scratch_get(vct_ctx* c, int i, size_t bytes, void** out) {
+    Scratch& s = c->scratch[i];
+    if (s.bytes < bytes) {
+        if (s.p) {
+            hipError_t e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess) return e;
+            (void)hipFree(s.p);
+            s.p = nullptr;
+            s.bytes = 0;
+        }
+        hipError_t e = hipMalloc(&s.p, bytes);
+        if (e != hipSuccess) return e;
+        s.bytes = bytes;
+    }
+    *out = s.p;
+    return hipSuccess;
+}
+}  // namespace vct
+
+extern "C" {
+
+uint32_t vct_abi_version(void) { return VCT_ABI_VERSION; }
+
+const char* vct_status_string(vct_status s) {
+    switch (s) {
+        case VCT_OK: return "VCT_OK";
+        case VCT_EINVAL: return "VCT_EINVAL";
+        case VCT_ENOMEM: return "VCT_ENOMEM";
+        case VCT_EDEVICE: return "VCT_EDEVICE";
+        case VCT_ECOMM: return "VCT_ECOMM";
+        case VCT_ESTATE: return "VCT_ESTATE";
+    }
+    return "VCT_UNKNOWN";
+}
+
+const char* vct_last_error(const vct_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
+    if (!cfg || !out) return VCT_EINVAL;
+    *out = nullptr;
+    if (!is_pow2(cfg->n) || cfg->n < 4 || cfg->n > 1024) return VCT_EINVAL;
+    if (!(cfg->extent > 0.0f) || !std::isfinite(cfg->extent)) return VCT_EINVAL;
+    if (cfg->n_diffuse != 0 && cfg->n_diffuse != 1 && cfg->n_diffuse != 9 && cfg->n_diffuse != 16)
+        return VCT_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VCT_EDEVICE;
+    int dev = cfg->device;
+    if (dev < 0) {
+        if (hipGetDevice(&dev) != hipSuccess) return VCT_EDEVICE;
+    }
+    if (dev >= ndev) return VCT_EINVAL;
+    vct_ctx* c = new (std::nothrow) vct_ctx();
+    if (!c) return VCT_ENOMEM;
+    c->cfg = *cfg;
+    c->device = dev;
+    c->cfg.device = dev;
+    if (hipSetDevice(dev) != hipSuccess) { delete c; return VCT_EDEVICE; }
+    Grid& g = c->grid;
+    g.n = cfg->n;
+    g.L = ilog2u(cfg->n);
+    g.aniso = cfg->aniso ? 1 : 0;
+    for (int i = 0; i < 3; ++i) g.g0[i] = cfg->aabb_min[i];
+    g.extent = cfg->extent;
+    g.inv_h = (float)cfg->n / cfg->extent;
+    const uint64_t faces = g.aniso ? VCT_NUM_FACES : 1;
+    uint64_t off = 0;
+    for (uint32_t l = 0; l <= g.L; ++l) {
+        g.lvl_off[l] = off;
+        const uint64_t nl = g.n >> l;
+        off += (l == 0 ? 1 : faces) * nl * nl * nl;
+    }
+    for (uint32_t l = g.L + 1; l <= (uint32_t)kMaxLevels; ++l) g.lvl_off[l] = off;
+    g.pyr_texels = off;
+    const size_t nv = (size_t)g.n * g.n * g.n;
+    hipError_t e = hipMalloc(&g.pyr, off * sizeof(float4));
+    if (e == hipSuccess) e = hipMemset(g.pyr, 0, off * sizeof(float4));
+    if (e == hipSuccess) e = hipMalloc(&g.albedo_occ, nv * sizeof(float4));
+    if (e == hipSuccess) e = hipMalloc(&g.normal, nv * sizeof(float4));
+    if (e == hipSuccess) e = hipMalloc(&g.occ_bits, (nv / 64) * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&g.accum, nv * 64);
+    if (e != hipSuccess) {
+        vct_destroy(c);
+        return e == hipErrorOutOfMemory ? VCT_ENOMEM : VCT_EDEVICE;
+    }
+    *out = c;
+    return VCT_OK;
+}
+
+void vct_destroy(vct_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    else (void)hipDeviceSynchronize();
+    Grid& g = c->grid;
+    if (g.pyr) (void)hipFree(g.pyr);
+    if (g.albedo_occ) (void)hipFree(g.albedo_occ);
+    if (g.normal) (void)hipFree(g.normal);
+    if (g.occ_bits) (void)hipFree(g.occ_bits);
+    if (g.accum) (void)hipFree(g.accum);
+    if (c->mesh.tri) (void)hipFree(c->mesh.tri);
+    for (auto& s : c->scratch)
+        if (s.p) (void)hipFree(s.p);
+    delete c;
+}
+
+vct_status vct_get_config(const vct_ctx* c, vct_config* out) {
+    if (!c || !out) return VCT_EINVAL;
+    *out = c->cfg;
+    return VCT_OK;
+}
+
+vct_status vct_set_stream(vct_ctx* c, void* stream) {
+    if (!c) return VCT_EINVAL;
+    c->stream = (hipStream_t)stream;
+    return VCT_OK;
+}
+
+vct_status vct_synchronize(vct_ctx* c) {
+    if (!c) return VCT_EINVAL;
+    vct_status s = use_device(c);
+    if (s != VCT_OK) return s;
+    VCT_HIP(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    return VCT_OK;
+}
+
+vct_status vct_voxelize(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                        const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
+                        const float* kd4, uint32_t n_mat) {
+    if (!c) return VCT_EINVAL;
+    if (n_idx % 3 != 0) return fail(c, VCT_EINVAL, "n_idx must be a multiple of 3");
+    if (n_idx > 0 && (!verts || !idx)) return fail(c, VCT_EINVAL, "null vertex or index array");
+    if (stride < 12) return fail(c, VCT_EINVAL, "vertex_stride < 12");
+    if (kd4 && n_mat == 0) return fail(c, VCT_EINVAL, "material_kd4 with n_materials == 0");
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    const uint32_t n_tri = n_idx / 3;
+    // host -> device staging (the reference keeps CPU copies of vertices / indices
+    // next to its GL buffers, mesh.h:17-18; this is the same one-time upload)
+    DeviceBuf dv, di, dm, dk, derr;
+    const size_t vbytes = (size_t)stride * n_verts;
+    if (vbytes) VCT_HIP(hipMalloc(&dv.p, vbytes), "hipMalloc verts");
+    if (n_idx) VCT_HIP(hipMalloc(&di.p, (size_t)n_idx * 4), "hipMalloc idx");
+    if (tri_mat && n_tri) VCT_HIP(hipMalloc(&dm.p, (size_t)n_tri * 4), "hipMalloc mat");
+    if (kd4) VCT_HIP(hipMalloc(&dk.p, (size_t)n_mat * 16), "hipMalloc kd");
+    VCT_HIP(hipMalloc(&derr.p, 4), "hipMalloc err");
+    if (vbytes) VCT_HIP(hipMemcpyAsync(dv.p, verts, vbytes, hipMemcpyHostToDevice, c->stream), "upload verts");
+    if (n_idx) VCT_HIP(hipMemcpyAsync(di.p, idx, (size_t)n_idx * 4, hipMemcpyHostToDevice, c->stream), "upload idx");
+    if (dm.p) VCT_HIP(hipMemcpyAsync(dm.p, tri_mat, (size_t)n_tri * 4, hipMemcpyHostToDevice, c->stream), "upload mat");
+    if (dk.p) VCT_HIP(hipMemcpyAsync(dk.p, kd4, (size_t)n_mat * 16, hipMemcpyHostToDevice, c->stream), "upload kd");
+    VCT_HIP(hipMemsetAsync(derr.p, 0, 4, c->stream), "memset err");
+    Mesh& m = c->mesh;
+    const size_t tri_bytes = (size_t)(n_tri ? n_tri : 1) * 4 * sizeof(float4);
+    if (m.cap < tri_bytes) {
+        VCT_HIP(hipStreamSynchronize(c->stream), "sync");
+        if (m.tri) (void)hipFree(m.tri);
+        m.tri = nullptr;
+        m.cap = 0;
+        VCT_HIP(hipMalloc(&m.tri, tri_bytes), "hipMalloc mesh");
+        m.cap = tri_bytes;
+    }
+    m.n_tri = n_tri;
+    VCT_HIP(launch_voxelize(c, dv.p, stride, n_verts, (const uint32_t*)di.p, n_tri,
+                            (const uint32_t*)dm.p, (const float4*)dk.p, n_mat, (int*)derr.p),
+            "voxelize");
+    int herr = 0;
+    VCT_HIP(hipMemcpyAsync(&herr, derr.p, 4, hipMemcpyDeviceToHost, c->stream), "download err");
+    VCT_HIP(hipStreamSynchronize(c->stream), "voxelize sync");
+    c->grid.voxelized = true;
+    c->grid.injected = c->grid.mipped = false;
+    if (herr) return fail(c, VCT_EINVAL, "vertex or material index out of range");
+    return VCT_OK;
+}
+
+vct_status vct_inject_directional(vct_ctx* c, const float dir[3], const float color[3]) {
+    if (!c || !dir || !color) return VCT_EINVAL;
+    if (!c->grid.voxelized) return fail(c, VCT_ESTATE, "inject before voxelize");
+    float lx = dir[0], ly = dir[1], lz = dir[2];
+    const float len = sqrtf((lx * lx + ly * ly) + lz * lz);
+    if (!(len > 0.0f) || !std::isfinite(len)) return fail(c, VCT_EINVAL, "zero or non-finite light direction");
+    lx = lx / len; ly = ly / len; lz = lz / len;
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(launch_inject(c, lx, ly, lz, color[0], color[1], color[2]), "inject");
+    c->grid.injected = true;
+    c->grid.mipped = false;
+    return VCT_OK;
+}
+
+vct_status vct_build_mips(vct_ctx* c) {
+    if (!c) return VCT_EINVAL;
+    if (!c->grid.injected) return fail(c, VCT_ESTATE, "build_mips before inject / upload_level0");
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(launch_mips(c), "mips");
+    c->grid.mipped = true;
+    return VCT_OK;
+}
+
+uint32_t vct_tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
+    return tiles_for_rank(w, h, rank, world);
+}
+
+vct_status vct_trace_device(vct_ctx* c, const vct_trace_args* a) {
+    if (!c || !a) return VCT_EINVAL;
+    if (!c->grid.mipped) return fail(c, VCT_ESTATE, "trace before build_mips");
+    if (!a->pos4 || !a->nrm4 || !a->alb4 || !a->diffuse4 || !a->spec4)
+        return fail(c, VCT_EINVAL, "null G-buffer or output pointer");
+    if (a->width == 0 || a->height == 0 || a->width > 65536 || a->height > 65536)
+        return fail(c, VCT_EINVAL, "bad frame size");
+    if (a->tile_world > 1 && a->tile_rank >= a->tile_world) return fail(c, VCT_EINVAL, "tile_rank >= tile_world");
+    // the counters are 64-bit device atomics: a misaligned target faults the GPU
+    if (((uintptr_t)a->cone_steps & 7) || ((uintptr_t)a->texel_fetches & 7))
+        return fail(c, VCT_EINVAL, "cone_steps / texel_fetches must be 8-byte aligned");
+    if (((uintptr_t)a->pos4 | (uintptr_t)a->nrm4 | (uintptr_t)a->alb4 | (uintptr_t)a->diffuse4 |
+         (uintptr_t)a->spec4) & 15)
+        return fail(c, VCT_EINVAL, "G-buffer / output pointers must be 16-byte aligned");
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(launch_trace(c, a), "trace");
+    return VCT_OK;
+}
+
+vct_status vct_trace(vct_ctx* c, const float* pos4, const float* nrm4, const float* alb4, uint32_t w,
+                     uint32_t h, const float eye[3], float* diff4, float* spec4, uint32_t* steps_px,
+                     uint64_t* cone_steps) {
+    if (!c || !pos4 || !nrm4 || !alb4 || !eye || !diff4 || !spec4) return VCT_EINVAL;
+    if (!c->grid.mipped) return fail(c, VCT_ESTATE, "trace before build_mips");
+    if (w == 0 || h == 0) return fail(c, VCT_EINVAL, "bad frame size");
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    // every sub-buffer 256-byte aligned (the u64 step counter is an atomic target)
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t px = (size_t)w * h, fb = al(px * 16), sb = al(px * 4);
+    void* sp;
+    VCT_HIP(scratch_get(c, 0, fb * 5 + sb + 256, &sp), "scratch");
+    char* b = (char*)sp;
+    float* dpos = (float*)b;
+    float* dnrm = (float*)(b + fb);
+    float* dalb = (float*)(b + 2 * fb);
+    float* ddif = (float*)(b + 3 * fb);
+    float* dspc = (float*)(b + 4 * fb);
+    uint32_t* dstp = (uint32_t*)(b + 5 * fb);
+    unsigned long long* dtot = (unsigned long long*)(b + 5 * fb + sb);
+    VCT_HIP(hipMemcpyAsync(dpos, pos4, px * 16, hipMemcpyHostToDevice, c->stream), "upload pos");
+    VCT_HIP(hipMemcpyAsync(dnrm, nrm4, px * 16, hipMemcpyHostToDevice, c->stream), "upload nrm");
+    VCT_HIP(hipMemcpyAsync(dalb, alb4, px * 16, hipMemcpyHostToDevice, c->stream), "upload alb");
+    VCT_HIP(hipMemsetAsync(dtot, 0, 8, c->stream), "memset");
+    vct_trace_args a;
+    std::memset(&a, 0, sizeof a);
+    a.pos4 = dpos; a.nrm4 = dnrm; a.alb4 = dalb;
+    a.width = w; a.height = h;
+    a.eye[0] = eye[0]; a.eye[1] = eye[1]; a.eye[2] = eye[2];
+    a.diffuse4 = ddif; a.spec4 = dspc;
+    a.steps_px = steps_px ? dstp : nullptr;
+    a.cone_steps = dtot;
+    VCT_HIP(launch_trace(c, &a), "trace");
+    VCT_HIP(hipMemcpyAsync(diff4, ddif, px * 16, hipMemcpyDeviceToHost, c->stream), "download diffuse");
+    VCT_HIP(hipMemcpyAsync(spec4, dspc, px * 16, hipMemcpyDeviceToHost, c->stream), "download spec");
+    if (steps_px) VCT_HIP(hipMemcpyAsync(steps_px, dstp, px * 4, hipMemcpyDeviceToHost, c->stream), "download steps");
+    unsigned long long tot = 0;
+    VCT_HIP(hipMemcpyAsync(&tot, dtot, 8, hipMemcpyDeviceToHost, c->stream), "download total");
+    VCT_HIP(hipStreamSynchronize(c->stream), "trace sync");
+    if (cone_steps) *cone_steps = tot;
+    return VCT_OK;
+}
+
+vct_status vct_untile_device(vct_ctx* c, const float* gathered4, uint32_t w, uint32_t h, uint32_t world,
+                             float* frame4) {
+    if (!c || !gathered4 || !frame4 || w == 0 || h == 0) return VCT_EINVAL;
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(launch_untile(c, (const float4*)gathered4, w, h, world, (float4*)frame4), "untile");
+    return VCT_OK;
+}
+
+vct_status vct_gbuffer_raycast_device(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h,
+                                      float rough, float* pos4, float* nrm4, float* alb4) {
+    if (!c || !cam || !pos4 || !nrm4 || !alb4 || w == 0 || h == 0) return VCT_EINVAL;
+    if (!c->mesh.tri) return fail(c, VCT_ESTATE, "raycast before voxelize");
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(launch_raycast(c, cam, w, h, rough, (float4*)pos4, (float4*)nrm4, (float4*)alb4), "raycast");
+    return VCT_OK;
+}
+
+vct_status vct_device_alloc(vct_ctx* c, size_t bytes, void** dptr) {
+    if (!c || !dptr || bytes == 0) return VCT_EINVAL;
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(hipMalloc(dptr, bytes), "hipMalloc");
+    return VCT_OK;
+}
+
+vct_status vct_device_free(vct_ctx* c, void* dptr) {
+    if (!c) return VCT_EINVAL;
+    if (!dptr) return VCT_OK;
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(hipFree(dptr), "hipFree");
+    return VCT_OK;
+}
+
+vct_status vct_memcpy(vct_ctx* c, void* dst, const void* src, size_t bytes, int kind) {
+    if (!c || (!dst && bytes) || (!src && bytes) || kind < 0 || kind > 2) return VCT_EINVAL;
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                          : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
+    VCT_HIP(hipMemcpyAsync(dst, src, bytes, k, c->stream), "memcpy");
+    VCT_HIP(hipStreamSynchronize(c->stream), "memcpy sync");
+    return VCT_OK;
+}
+
+uint32_t vct_num_levels(const vct_ctx* c) { return c ? c->grid.L + 1 : 0; }
+
+vct_status vct_level_dims(const vct_ctx* c, uint32_t level, uint32_t* n_l, uint32_t* n_faces) {
+    if (!c || level > c->grid.L) return VCT_EINVAL;
+    if (n_l) *n_l = c->grid.n >> level;
+    if (n_faces) *n_faces = (level == 0 || !c->grid.aniso) ? 1 : VCT_NUM_FACES;
+    return VCT_OK;
+}
+
+vct_status vct_download_level(vct_ctx* c, uint32_t level, uint32_t face, float* host) {
+    if (!c || !host || level > c->grid.L) return VCT_EINVAL;
+    const uint32_t faces = (level == 0 || !c->grid.aniso) ? 1 : VCT_NUM_FACES;
+    if (face >= faces) return fail(c, VCT_EINVAL, "face out of range for level");
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    const size_t nl = c->grid.n >> level, vl = nl * nl * nl;
+    const float4* src = c->grid.pyr + c->grid.lvl_off[level] + face * vl;
+    VCT_HIP(hipMemcpyAsync(host, src, vl * 16, hipMemcpyDeviceToHost, c->stream), "download level");
+    VCT_HIP(hipStreamSynchronize(c->stream), "sync");
+    return VCT_OK;
+}
+
+vct_status vct_upload_level0(vct_ctx* c, const float* host) {
+    if (!c || !host) return VCT_EINVAL;
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    const size_t nv = (size_t)c->grid.n * c->grid.n * c->grid.n;
+    VCT_HIP(hipMemcpyAsync(c->grid.pyr, host, nv * 16, hipMemcpyHostToDevice, c->stream), "upload level0");
+    VCT_HIP(hipStreamSynchronize(c->stream), "sync");
+    c->grid.injected = true;
+    c->grid.mipped = false;
+    return VCT_OK;
+}
+
+vct_status vct_level0_device(vct_ctx* c, void** dptr, size_t* bytes) {
+    if (!c || !dptr) return VCT_EINVAL;
+    *dptr = c->grid.pyr;
+    if (bytes) *bytes = (size_t)c->grid.n * c->grid.n * c->grid.n * 16;
+    // the caller (e.g. an RCCL broadcast) writes level 0 behind our back
+    c->grid.injected = true;
+    c->grid.mipped = false;
+    return VCT_OK;
+}
+
+vct_status vct_copy_level0_to_device(vct_ctx* c, void* dst) {
+    if (!c || !dst) return VCT_EINVAL;
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    const size_t nv = (size_t)c->grid.n * c->grid.n * c->grid.n;
+    VCT_HIP(hipMemcpyAsync(dst, c->grid.pyr, nv * 16, hipMemcpyDeviceToDevice, c->stream), "copy level0 out");
+    return VCT_OK;
+}
+
+vct_status vct_set_level0_from_device(vct_ctx* c, const void* src) {
+    if (!c || !src) return VCT_EINVAL;
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    const size_t nv = (size_t)c->grid.n * c->grid.n * c->grid.n;
+    VCT_HIP(hipMemcpyAsync(c->grid.pyr, src, nv * 16, hipMemcpyDeviceToDevice, c->stream), "copy level0 in");
+    c->grid.injected = true;
+    c->grid.mipped = false;
+    return VCT_OK;
+}
+
+vct_status vct_download_voxels(vct_ctx* c, float* albedo_occ4, float* normal4) {
+    if (!c) return VCT_EINVAL;
+    if (!c->grid.voxelized) return fail(c, VCT_ESTATE, "download_voxels before voxelize");
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    const size_t nv = (size_t)c->grid.n * c->grid.n * c->grid.n;
+    if (albedo_occ4) VCT_HIP(hipMemcpyAsync(albedo_occ4, c->grid.albedo_occ, nv * 16, hipMemcpyDeviceToHost, c->stream), "download albedo");
+    if (normal4) VCT_HIP(hipMemcpyAsync(normal4, c->grid.normal, nv * 16, hipMemcpyDeviceToHost, c->stream), "download normal");
+    VCT_HIP(hipStreamSynchronize(c->stream), "sync");
+    return VCT_OK;
+}
+
+vct_status vct_download_accum(vct_ctx* c, int64_t* sums6, uint32_t* counts) {
+    if (!c) return VCT_EINVAL;
+    if (!c->grid.voxelized) return fail(c, VCT_ESTATE, "download_accum before voxelize");
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    const size_t nv = (size_t)c->grid.n * c->grid.n * c->grid.n;
+    // stage the [n^3][8] records through a host buffer, then split
+    long long* tmp = new (std::nothrow) long long[nv * 8];
+    if (!tmp) return fail(c, VCT_ENOMEM, "host staging");
+    hipError_t e = hipMemcpyAsync(tmp, c->grid.accum, nv * 64, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) { delete[] tmp; return hip_fail(c, e, "download accum"); }
+    for (size_t v = 0; v < nv; ++v) {
+        if (sums6)
+            for (int k = 0; k < 6; ++k) sums6[6 * v + k] = tmp[8 * v + k];
+        if (counts) counts[v] = (uint32_t)tmp[8 * v + 6];
+    }
+    delete[] tmp;
+    return VCT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,44 @@
+// vct_device.h — device-side spec math shared by the HIP kernels (gfx950).
+//
+// Every routine here is the device form of a rule of SURVEY.md Appendix A as
+// pinned by include/vct_spec.h.  The translation units are compiled with
+// -ffp-contract=off, so the operation sequence written here is the one that
+// executes; the explicit fmaf() calls are the spec's fused operations.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/vct_spec.h"
+
+namespace vct {
+
+constexpr int kMaxLevels = 11;  // n <= 1024 -> L <= 10
+
+// A.6 mip level m = log2(D), D >= 1 (vct_spec.h VCT_LOG2_*).
+__device__ __forceinline__ float spec_log2(float x) {
+    uint32_t bits = __float_as_uint(x);
+    int e = (int)((bits >> 23) & 0xffu) - 127;
+    float f = __uint_as_float((bits & 0x007fffffu) | 0x3f800000u);
+    if (f > VCT_LOG2_SQRT2) { f = f * 0.5f; e += 1; }
+    float s = (f - 1.0f) / (f + 1.0f);
+    float z = s * s;
+    float p = VCT_LOG2_C9;
+    p = fmaf(p, z, VCT_LOG2_C7);
+    p = fmaf(p, z, VCT_LOG2_C5);
+    p = fmaf(p, z, VCT_LOG2_C3);
+    p = fmaf(p, z, 1.0f);
+    float ln = (2.0f * s) * p;
+    return fmaf(ln, VCT_INV_LN2, (float)e);
+}
+
+__device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
+    return (ax * bx + ay * by) + az * bz;
+}
+
+// 64-lane wave sum (wave64 on CDNA: 6 butterfly steps)
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+}  // namespace vct

@@ -1,0 +1,78 @@
+// vct_internal.h — context object and kernel launchers behind include/vct.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include "../../include/vct.h"
+#include "vct_device.h"
+
+namespace vct {
+
+// Device-resident state of one context.  Everything lives in HBM for the life
+// of the context; nothing is re-allocated per frame.
+struct Grid {
+    uint32_t n = 0, L = 0;
+    int aniso = 1;
+    float g0[3] = {0, 0, 0};
+    float extent = 1.0f;
+    float inv_h = 1.0f;
+    // radiance pyramid: ONE allocation, level 0 (isotropic) then levels 1..L,
+    // each level = faces x n_l^3 float4 texels, linear-Z inside a face volume.
+    float4* pyr = nullptr;
+    uint64_t lvl_off[kMaxLevels + 1] = {};   // float4 offset of each level
+    uint64_t pyr_texels = 0;
+    // K1 state
+    long long* accum = nullptr;      // [n^3][8] int64: albedo rgb, normal xyz, count, pad
+    float4* albedo_occ = nullptr;    // [n^3] (albedo rgb, occupancy)
+    float4* normal = nullptr;        // [n^3] (unit normal, 0)
+    unsigned long long* occ_bits = nullptr;  // [n^3 / 64] occupancy bitmask
+    bool voxelized = false, injected = false, mipped = false;
+};
+
+struct Mesh {
+    float4* tri = nullptr;        // [n_tri][4] : v0, e1 = v1-v0, e2 = v2-v0, (kd rgb, 0)
+    uint32_t n_tri = 0;
+    size_t cap = 0;
+};
+
+struct Scratch {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace vct
+
+struct vct_ctx {
+    vct_config cfg{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    vct::Grid grid;
+    vct::Mesh mesh;
+    vct::Scratch scratch[4];      // reusable scratch (trace host staging, voxelize temps)
+    std::string err;
+};
+
+namespace vct {
+
+// K1
+hipError_t launch_voxelize(vct_ctx* c, const void* d_verts,
+                           uint32_t stride, uint32_t n_verts, const uint32_t* d_idx, uint32_t n_tri,
+                           const uint32_t* d_mat, const float4* d_kd, uint32_t n_mat, int* d_err);
+// K2
+hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb);
+// K3
+hipError_t launch_mips(vct_ctx* c);
+// K4
+hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a);
+hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t w, uint32_t h, uint32_t world,
+                         float4* frame);
+// G-buffer
+hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
+                          float4* pos, float4* nrm, float4* alb);
+
+uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world);
+
+// scratch helper: grows scratch slot `i` to at least `bytes`
+hipError_t scratch_get(vct_ctx* c, int i, size_t bytes, void** out);
+
+}  // namespace vct

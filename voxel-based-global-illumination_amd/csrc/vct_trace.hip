@@ -1,0 +1,395 @@
+// vct_trace.hip — K4 per-pixel diffuse + specular cone trace (the metric kernel),
+// the multi-GPU tile un-permute, and the G-buffer ray caster.
+//
+// SURVEY.md Appendix A.5 / A.6.  The reference has no cone tracer: its only GPU
+// program is the forward textured draw of assets/code/shader/test.{vert,frag},
+// invoked by VoxelizationRenderer::Render (assets/code/renderer/r_voxelization.cpp:4-35).
+//
+// MI355X design of K4 (memory-gather bound, no MFMA):
+//  * one lane = one pixel; a 64-lane wave is an 8x8 pixel block and a
+//    256-thread workgroup a 16x16 block, so a wave's cones start at nearly the
+//    same voxel and march in nearly the same direction: the texel footprint of
+//    the 64 lanes overlaps heavily and is served from the CU's L1 / the XCD's L2;
+//  * the screen is cut into 64x64 tiles; tile t belongs to rank t % world
+//    (SURVEY 8e), and inside a rank the workgroup -> tile map is XCD-aware: the
+//    eight round-robin XCD groups each get one contiguous run of tiles, so
+//    neighbouring workgroups (which gather the same bricks) share an L2;
+//  * diffuse cones have a wave-uniform step sequence (t, D and the mip pair
+//    depend only on tau), so the level branch is uniform and the per-lane
+//    early-out (a >= 0.95, left the grid) only masks lanes;
+//  * texels are 16-byte RGBA32F gathers (global_load_dwordx4), zero border by
+//    zeroed weights on clamped addresses (no out-of-bounds access, no branch).
+#include "vct_internal.h"
+
+namespace vct {
+namespace {
+
+#define VCT_CROW(cn, ct, cb, w) {cn, ct, cb, w},
+__constant__ float c_cones1[1][4] = {VCT_CONES1(VCT_CROW)};
+__constant__ float c_cones9[9][4] = {VCT_CONES9(VCT_CROW)};
+__constant__ float c_cones16[16][4] = {VCT_CONES16(VCT_CROW)};
+
+struct TraceK {
+    const float4* pyr;
+    uint64_t lvl_off[kMaxLevels + 1];
+    int n, L;
+    float g0x, g0y, g0z, inv_h, tmax;
+    const float4* pos;
+    const float4* nrm;
+    const float4* alb;
+    float4* diff;
+    float4* spec;
+    uint32_t* steps_px;
+    unsigned long long* steps_total;
+    unsigned long long* texels_total;
+    int w, h;
+    float ex, ey, ez;
+    int tiles_x, rank, world, n_local_tiles, compact;
+    int nd, spec_on, aniso;
+    float tau_d;
+};
+
+// trilinear weights + clamped corner indices of one level (GL texel centres)
+struct Tri {
+    uint32_t i[8];
+    float wc[8];
+};
+
+__device__ __forceinline__ void tri_setup(int nl, float cx, float cy, float cz, Tri& t) {
+    float fx0 = floorf(cx), fy0 = floorf(cy), fz0 = floorf(cz);
+    int ix = (int)fx0, iy = (int)fy0, iz = (int)fz0;
+    float fx = cx - fx0, fy = cy - fy0, fz = cz - fz0;
+    float wx[2] = {1.0f - fx, fx}, wy[2] = {1.0f - fy, fy}, wz[2] = {1.0f - fz, fz};
+    int xs[2] = {ix, ix + 1}, ys[2] = {iy, iy + 1}, zs[2] = {iz, iz + 1};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if ((unsigned)xs[k] >= (unsigned)nl) { wx[k] = 0.0f; xs[k] = 0; }
+        if ((unsigned)ys[k] >= (unsigned)nl) { wy[k] = 0.0f; ys[k] = 0; }
+        if ((unsigned)zs[k] >= (unsigned)nl) { wz[k] = 0.0f; zs[k] = 0; }
+    }
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+                const int c = dz * 4 + dy * 2 + dx;
+                t.i[c] = (uint32_t)xs[dx] + (uint32_t)nl * ((uint32_t)ys[dy] + (uint32_t)nl * (uint32_t)zs[dz]);
+                t.wc[c] = (wx[dx] * wy[dy]) * wz[dz];
+            }
+}
+
+__device__ __forceinline__ float4 tri_gather(const float4* __restrict__ vol, const Tri& t) {
+    float4 v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = vol[t.i[c]];
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        acc.x = fmaf(t.wc[c], v[c].x, acc.x);
+        acc.y = fmaf(t.wc[c], v[c].y, acc.y);
+        acc.z = fmaf(t.wc[c], v[c].z, acc.z);
+        acc.w = fmaf(t.wc[c], v[c].w, acc.w);
+    }
+    return acc;
+}
+
+// D_l(q, d) (A.5): level 0 isotropic, level >= 1 directional over 3 faces
+__device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx, float qy, float qz,
+                                               int fx, int fy, int fz, float wdx, float wdy, float wdz) {
+    const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
+    const int nl = k.n >> l;
+    Tri t;
+    tri_setup(nl, qx * scale - 0.5f, qy * scale - 0.5f, qz * scale - 0.5f, t);
+    const float4* lvl = k.pyr + k.lvl_off[l];
+    if (l == 0 || !k.aniso) return tri_gather(lvl, t);
+    const size_t vl = (size_t)nl * nl * nl;
+    float4 tx = tri_gather(lvl + (size_t)fx * vl, t);
+    float4 ty = tri_gather(lvl + (size_t)fy * vl, t);
+    float4 tz = tri_gather(lvl + (size_t)fz * vl, t);
+    float4 s;
+    s.x = fmaf(wdz, tz.x, fmaf(wdy, ty.x, wdx * tx.x));
+    s.y = fmaf(wdz, tz.y, fmaf(wdy, ty.y, wdx * tx.y));
+    s.z = fmaf(wdz, tz.z, fmaf(wdy, ty.z, wdx * tx.z));
+    s.w = fmaf(wdz, tz.w, fmaf(wdy, ty.w, wdx * tx.w));
+    return s;
+}
+
+// one cone (A.6); returns steps, accumulates (c, a) into res
+__device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, float oz, float dx,
+                                          float dy, float dz, float tau, float4& res, uint32_t& texels) {
+    const float tau2 = 2.0f * tau;
+    const float nf = (float)k.n, Lf = (float)k.L;
+    const int fx = dx >= 0.0f ? VCT_FACE_PX : VCT_FACE_NX;
+    const int fy = dy >= 0.0f ? VCT_FACE_PY : VCT_FACE_NY;
+    const int fz = dz >= 0.0f ? VCT_FACE_PZ : VCT_FACE_NZ;
+    const float wdx = dx * dx, wdy = dy * dy, wdz = dz * dz;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f, a = 0.0f, t = 1.0f;
+    uint32_t steps = 0;
+    for (;;) {
+        if (!(a < VCT_ALPHA_STOP)) break;
+        if (!(t <= k.tmax)) break;
+        const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
+        if (!(qx >= 0.0f && qx <= nf && qy >= 0.0f && qy <= nf && qz >= 0.0f && qz <= nf)) break;
+        const float D = fmaxf(1.0f, tau2 * t);
+        float m = spec_log2(D);
+        if (m > Lf) m = Lf;
+        const int l0 = (int)m;
+        const float fr = m - (float)l0;
+        float4 s = sample_level(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+        texels += (l0 == 0 || !k.aniso) ? 8u : 24u;
+        if (fr > 0.0f && l0 < k.L) {
+            texels += k.aniso ? 24u : 8u;
+            float4 s1 = sample_level(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+            const float omf = 1.0f - fr;
+            s.x = fmaf(fr, s1.x, omf * s.x);
+            s.y = fmaf(fr, s1.y, omf * s.y);
+            s.z = fmaf(fr, s1.z, omf * s.z);
+            s.w = fmaf(fr, s1.w, omf * s.w);
+        }
+        const float oma = 1.0f - a;
+        cr = fmaf(oma, s.x, cr);
+        cg = fmaf(oma, s.y, cg);
+        cb = fmaf(oma, s.z, cb);
+        a = fmaf(oma, s.w, a);
+        t = t + VCT_STEP_SCALE * D;
+        ++steps;
+    }
+    res = make_float4(cr, cg, cb, a);
+    return steps;
+}
+
+__device__ __forceinline__ const float (*cone_table(int nd))[4] {
+    return nd == 16 ? c_cones16 : (nd == 9 ? c_cones9 : c_cones1);
+}
+
+__global__ void __launch_bounds__(256) k4_trace(TraceK k) {
+    // XCD-aware workgroup -> (local tile, 16x16 block) map (bijective for any grid)
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const uint32_t xcd = b & 7, q = nb >> 3, r = nb & 7;
+    const uint32_t rb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    const uint32_t lt = rb >> 4, sub = rb & 15;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t px = (sub & 3) * 16 + (wave & 1) * 8 + (lane & 7);
+    const uint32_t py = (sub >> 2) * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const uint32_t tile = lt * (uint32_t)k.world + (uint32_t)k.rank;
+    const uint32_t x = (tile % (uint32_t)k.tiles_x) * VCT_TILE + px;
+    const uint32_t y = (tile / (uint32_t)k.tiles_x) * VCT_TILE + py;
+    const bool in_frame = x < (uint32_t)k.w && y < (uint32_t)k.h;
+    const size_t pix = (size_t)y * (size_t)k.w + x;
+    const size_t oidx = k.compact ? (size_t)lt * (VCT_TILE * VCT_TILE) + py * VCT_TILE + px : pix;
+
+    float4 dout = make_float4(0.0f, 0.0f, 0.0f, 0.0f), sout = dout;
+    uint32_t steps = 0, texels = 0;
+    float4 P = in_frame ? k.pos[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (P.w != 0.0f) {
+        const float4 N4 = k.nrm[pix];
+        const float nx = N4.x, ny = N4.y, nz = N4.z;
+        const float ox = (P.x - k.g0x) * k.inv_h + nx;
+        const float oy = (P.y - k.g0y) * k.inv_h + ny;
+        const float oz = (P.z - k.g0z) * k.inv_h + nz;
+        // Duff et al. 2017 branchless orthonormal basis
+        const float sgn = copysignf(1.0f, nz);
+        const float ka = -1.0f / (sgn + nz);
+        const float kb = (nx * ny) * ka;
+        const float Tx = 1.0f + ((sgn * nx) * nx) * ka, Ty = sgn * kb, Tz = -(sgn * nx);
+        const float Bx = kb, By = sgn + (ny * ny) * ka, Bz = -ny;
+        const float(*cones)[4] = cone_table(k.nd);
+        float ir = 0.0f, ig = 0.0f, ib = 0.0f, occ = 0.0f;
+        for (int c = 0; c < k.nd; ++c) {
+            const float cn = cones[c][0], ct = cones[c][1], cb = cones[c][2], wk = cones[c][3];
+            const float dx = (cn * nx + ct * Tx) + cb * Bx;
+            const float dy = (cn * ny + ct * Ty) + cb * By;
+            const float dz = (cn * nz + ct * Tz) + cb * Bz;
+            float4 res;
+            steps += march(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
+            ir = fmaf(wk, res.x, ir);
+            ig = fmaf(wk, res.y, ig);
+            ib = fmaf(wk, res.z, ib);
+            occ = fmaf(wk, res.w, occ);
+        }
+        dout = make_float4(ir, ig, ib, 1.0f - occ);
+        if (k.spec_on) {
+            float vx = k.ex - P.x, vy = k.ey - P.y, vz = k.ez - P.z;
+            const float vl = sqrtf(dot3(vx, vy, vz, vx, vy, vz));
+            vx = vx / vl; vy = vy / vl; vz = vz / vl;
+            const float ndv = dot3(nx, ny, nz, vx, vy, vz);
+            const float k2 = 2.0f * ndv;
+            const float rx = k2 * nx - vx, ry = k2 * ny - vy, rz = k2 * nz - vz;
+            const float tau = fminf(fmaxf(k.alb[pix].w, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
+            float4 res;
+            steps += march(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
+            sout = res;
+        }
+    }
+    if (in_frame || k.compact) {
+        k.diff[oidx] = dout;
+        k.spec[oidx] = sout;
+        if (k.steps_px && in_frame) k.steps_px[pix] = steps;
+    }
+    if (k.steps_total) {
+        uint32_t ws = wave_sum_u32(steps);
+        if (lane == 0 && ws) atomicAdd(k.steps_total, (unsigned long long)ws);
+    }
+    if (k.texels_total) {
+        uint32_t wt = wave_sum_u32(texels);
+        if (lane == 0 && wt) atomicAdd(k.texels_total, (unsigned long long)wt);
+    }
+}
+
+// [world][max_tiles][64*64] rank-compact tiles -> [h][w] frame
+__global__ void __launch_bounds__(256) k_untile(const float4* __restrict__ g, int w, int h, int world,
+                                                int tiles_x, int max_tiles, float4* __restrict__ frame) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= w || y >= h) return;
+    const int t = (y / VCT_TILE) * tiles_x + (x / VCT_TILE);
+    const int rank = t % world, lt = t / world;
+    const size_t src = ((size_t)rank * max_tiles + lt) * (VCT_TILE * VCT_TILE) +
+                       (size_t)(y % VCT_TILE) * VCT_TILE + (x % VCT_TILE);
+    frame[(size_t)y * w + x] = g[src];
+}
+
+// ---- G-buffer ray caster (input producer for synthetic scenes) -----------
+struct RayK {
+    const float4* tri;  // [n][4]: v0, e1, e2, kd
+    uint32_t n_tri;
+    int w, h;
+    float px, py, pz;
+    float fx, fy, fz, ux, uy, uz, rx, ry, rz;
+    float tan_half, aspect, near_p, far_p, rough;
+    float4* pos;
+    float4* nrm;
+    float4* alb;
+};
+
+constexpr int kRayChunk = 256;
+
+__global__ void __launch_bounds__(256) k_raycast(RayK k) {
+    __shared__ float4 sh[kRayChunk * 4];
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const float ndx = (2.0f * ((float)x + 0.5f) / (float)k.w - 1.0f) * k.tan_half * k.aspect;
+    const float ndy = (1.0f - 2.0f * ((float)y + 0.5f) / (float)k.h) * k.tan_half;
+    float dx = k.fx + ndx * k.rx + ndy * k.ux;
+    float dy = k.fy + ndx * k.ry + ndy * k.uy;
+    float dz = k.fz + ndx * k.rz + ndy * k.uz;
+    const float il = 1.0f / sqrtf(dot3(dx, dy, dz, dx, dy, dz));
+    dx *= il; dy *= il; dz *= il;
+    float best = __builtin_inff();
+    int hit = -1;
+    for (uint32_t base = 0; base < k.n_tri; base += kRayChunk) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < kRayChunk * 4; i += 256) {
+            uint32_t tri = base + i / 4;
+            sh[i] = tri < k.n_tri ? k.tri[(size_t)tri * 4 + (i & 3)] : make_float4(0, 0, 0, 0);
+        }
+        __syncthreads();
+        const uint32_t cnt = min((uint32_t)kRayChunk, k.n_tri - base);
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const float4 v0 = sh[4 * j], e1 = sh[4 * j + 1], e2 = sh[4 * j + 2];
+            const float pvx = dy * e2.z - dz * e2.y, pvy = dz * e2.x - dx * e2.z, pvz = dx * e2.y - dy * e2.x;
+            const float det = dot3(e1.x, e1.y, e1.z, pvx, pvy, pvz);
+            if (fabsf(det) < 1e-12f) continue;
+            const float inv = 1.0f / det;
+            const float tx = k.px - v0.x, ty = k.py - v0.y, tz = k.pz - v0.z;
+            const float u = dot3(tx, ty, tz, pvx, pvy, pvz) * inv;
+            if (u < 0.0f || u > 1.0f) continue;
+            const float qx = ty * e1.z - tz * e1.y, qy = tz * e1.x - tx * e1.z, qz = tx * e1.y - ty * e1.x;
+            const float v = dot3(dx, dy, dz, qx, qy, qz) * inv;
+            if (v < 0.0f || u + v > 1.0f) continue;
+            const float t = dot3(e2.x, e2.y, e2.z, qx, qy, qz) * inv;
+            if (t > 0.0f && t < best) { best = t; hit = (int)(base + j); }
+        }
+    }
+    if (x >= k.w || y >= k.h) return;
+    const size_t p = (size_t)y * k.w + x;
+    const float depth = best * dot3(dx, dy, dz, k.fx, k.fy, k.fz);
+    if (hit < 0 || depth < k.near_p || depth > k.far_p) {
+        k.pos[p] = make_float4(0, 0, 0, 0);
+        k.nrm[p] = make_float4(0, 0, 0, 0);
+        k.alb[p] = make_float4(0, 0, 0, k.rough);
+        return;
+    }
+    const float4 e1 = k.tri[(size_t)hit * 4 + 1], e2 = k.tri[(size_t)hit * 4 + 2], kd = k.tri[(size_t)hit * 4 + 3];
+    float nx = e1.y * e2.z - e1.z * e2.y, ny = e1.z * e2.x - e1.x * e2.z, nz = e1.x * e2.y - e1.y * e2.x;
+    const float nl = sqrtf(dot3(nx, ny, nz, nx, ny, nz));
+    nx /= nl; ny /= nl; nz /= nl;
+    if (dot3(nx, ny, nz, dx, dy, dz) > 0.0f) { nx = -nx; ny = -ny; nz = -nz; }
+    k.pos[p] = make_float4(k.px + dx * best, k.py + dy * best, k.pz + dz * best, 1.0f);
+    k.nrm[p] = make_float4(nx, ny, nz, 0.0f);
+    k.alb[p] = make_float4(kd.x, kd.y, kd.z, k.rough);
+}
+
+}  // namespace
+
+uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
+    if (world == 0) world = 1;
+    const uint32_t tx = (w + VCT_TILE - 1) / VCT_TILE, ty = (h + VCT_TILE - 1) / VCT_TILE;
+    const uint32_t total = tx * ty;
+    if (rank >= world || total <= rank) return 0;
+    return (total - rank + world - 1) / world;
+}
+
+hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
+    const Grid& g = c->grid;
+    TraceK k;
+    k.pyr = g.pyr;
+    for (int i = 0; i <= kMaxLevels; ++i) k.lvl_off[i] = g.lvl_off[i];
+    k.n = (int)g.n; k.L = (int)g.L;
+    k.g0x = g.g0[0]; k.g0y = g.g0[1]; k.g0z = g.g0[2];
+    k.inv_h = g.inv_h;
+    k.tmax = (float)g.n * VCT_SQRT3;
+    k.pos = (const float4*)a->pos4; k.nrm = (const float4*)a->nrm4; k.alb = (const float4*)a->alb4;
+    k.diff = (float4*)a->diffuse4; k.spec = (float4*)a->spec4;
+    k.steps_px = a->steps_px; k.steps_total = a->cone_steps; k.texels_total = a->texel_fetches;
+    k.w = (int)a->width; k.h = (int)a->height;
+    k.ex = a->eye[0]; k.ey = a->eye[1]; k.ez = a->eye[2];
+    const uint32_t world = a->tile_world ? a->tile_world : 1;
+    k.tiles_x = (int)((a->width + VCT_TILE - 1) / VCT_TILE);
+    k.rank = (int)(a->tile_world ? a->tile_rank : 0);
+    k.world = (int)world;
+    const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
+    k.n_local_tiles = (int)nlt;
+    k.compact = a->tile_compact ? 1 : 0;
+    k.nd = (int)c->cfg.n_diffuse;
+    k.spec_on = c->cfg.specular ? 1 : 0;
+    k.aniso = g.aniso;
+    k.tau_d = c->cfg.n_diffuse == 16 ? VCT_TAN20 : VCT_TAN30;
+    if (nlt == 0) return hipSuccess;
+    const uint32_t blocks = nlt * 16;
+    hipLaunchKernelGGL(k4_trace, dim3(blocks), dim3(256), 0, c->stream, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t w, uint32_t h, uint32_t world,
+                         float4* frame) {
+    if (world == 0) world = 1;
+    const int tiles_x = (int)((w + VCT_TILE - 1) / VCT_TILE);
+    const int max_tiles = (int)tiles_for_rank(w, h, 0, world);
+    dim3 grid((w + 15) / 16, (h + 15) / 16);
+    hipLaunchKernelGGL(k_untile, grid, dim3(256), 0, c->stream, gathered, (int)w, (int)h, (int)world,
+                       tiles_x, max_tiles, frame);
+    return hipGetLastError();
+}
+
+hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
+                          float4* pos, float4* nrm, float4* alb) {
+    RayK k;
+    k.tri = c->mesh.tri; k.n_tri = c->mesh.n_tri;
+    k.w = (int)w; k.h = (int)h;
+    k.px = cam->position[0]; k.py = cam->position[1]; k.pz = cam->position[2];
+    k.fx = cam->front[0]; k.fy = cam->front[1]; k.fz = cam->front[2];
+    k.ux = cam->up[0]; k.uy = cam->up[1]; k.uz = cam->up[2];
+    k.rx = cam->right[0]; k.ry = cam->right[1]; k.rz = cam->right[2];
+    k.tan_half = tanf(cam->zoom_deg * 0.5f * 3.14159265358979f / 180.0f);
+    k.aspect = (float)w / (float)h;
+    k.near_p = cam->near_plane; k.far_p = cam->far_plane;
+    k.rough = rough;
+    k.pos = pos; k.nrm = nrm; k.alb = alb;
+    dim3 grid((w + 15) / 16, (h + 15) / 16);
+    hipLaunchKernelGGL(k_raycast, grid, dim3(256), 0, c->stream, k);
+    return hipGetLastError();
+}
+
+}  // namespace vct

@@ -1,0 +1,411 @@
+// vct_voxelize.hip — K1 conservative voxelization + resolve, K2 light injection.
+//
+// SURVEY.md Appendix A.2 / A.3 (the reference has no implementation: its
+// VoxelizationProgram is empty, assets/code/program/p_voxelization.h:4-7).
+//
+// K1 design (MI355X): triangles are flattened into a balanced 1-D work list of
+// (triangle, candidate voxel) pairs: a per-triangle candidate count, a device
+// exclusive scan, then one lane per candidate running the exact 13-axis SAT
+// test.  A few huge triangles (a Cornell wall covers n^2 voxels) therefore
+// spread over the whole chip instead of serialising one wave.  Coverage is
+// accumulated with 64-bit integer atomics on 16.16 fixed-point values, so the
+// result is independent of atomic arrival order: bit-exact and reproducible.
+// Per-voxel accumulators are 64-byte records [albedo rgb, normal xyz, count,
+// pad] so a voxel's seven atomics land in one half cache line.
+#include "vct_internal.h"
+
+namespace vct {
+namespace {
+
+struct TriGeom {      // 64 B
+    float q[9];       // voxel-unit vertex positions
+    int lo[3];        // first candidate voxel per axis
+    uint32_t ext[3];  // candidate extent per axis (0 = no candidates)
+    uint32_t pad;
+};
+struct TriFix {       // 64 B
+    long long fix[6]; // albedo rgb, face normal xyz in 16.16 fixed point
+    long long pad[2];
+};
+
+__device__ __forceinline__ float fmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
+__device__ __forceinline__ float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+
+__device__ __forceinline__ void cand_range(float mn, float mx, int n, int& lo, int& hi) {
+    int l = (int)ceilf(fmaxf(mn, -1.0f)) - 1;
+    int h = (int)floorf(fminf(mx, (float)n + 1.0f));
+    lo = l < 0 ? 0 : l;
+    hi = h > n - 1 ? n - 1 : h;
+}
+
+__global__ void __launch_bounds__(256) k1_tri_setup(
+    const char* __restrict__ verts, uint32_t stride, uint32_t n_verts,
+    const uint32_t* __restrict__ idx, uint32_t n_tri, const uint32_t* __restrict__ mat,
+    const float4* __restrict__ kd, uint32_t n_mat, int n, float g0x, float g0y, float g0z,
+    float inv_h, TriGeom* __restrict__ geom, TriFix* __restrict__ fixo,
+    unsigned long long* __restrict__ counts, float4* __restrict__ mesh_tri, int* __restrict__ err) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tri) return;
+    uint32_t vi[3] = {idx[3 * t], idx[3 * t + 1], idx[3 * t + 2]};
+    uint32_t m = mat ? mat[t] : 0u;
+    TriGeom g;
+    TriFix f;
+    if (vi[0] >= n_verts || vi[1] >= n_verts || vi[2] >= n_verts || (kd && m >= n_mat)) {
+        atomicOr(err, 1);
+        g.ext[0] = g.ext[1] = g.ext[2] = 0;
+        counts[t] = 0;
+        geom[t] = g;
+        return;
+    }
+    float p[3][3], q[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float* src = (const float*)(verts + (size_t)vi[k] * stride);
+        p[k][0] = src[0]; p[k][1] = src[1]; p[k][2] = src[2];
+        q[k][0] = (p[k][0] - g0x) * inv_h;
+        q[k][1] = (p[k][1] - g0y) * inv_h;
+        q[k][2] = (p[k][2] - g0z) * inv_h;
+        g.q[3 * k] = q[k][0]; g.q[3 * k + 1] = q[k][1]; g.q[3 * k + 2] = q[k][2];
+    }
+    float e1[3] = {p[1][0] - p[0][0], p[1][1] - p[0][1], p[1][2] - p[0][2]};
+    float e2[3] = {p[2][0] - p[0][0], p[2][1] - p[0][1], p[2][2] - p[0][2]};
+    float fn[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                   e1[0] * e2[1] - e1[1] * e2[0]};
+    float len = sqrtf(dot3(fn[0], fn[1], fn[2], fn[0], fn[1], fn[2]));
+    if (len > 0.0f) { fn[0] = fn[0] / len; fn[1] = fn[1] / len; fn[2] = fn[2] / len; }
+    else { fn[0] = 0.0f; fn[1] = 0.0f; fn[2] = 0.0f; }
+    float4 alb = kd ? kd[m] : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    f.fix[0] = (long long)roundf(alb.x * VCT_FIXED_ONE);
+    f.fix[1] = (long long)roundf(alb.y * VCT_FIXED_ONE);
+    f.fix[2] = (long long)roundf(alb.z * VCT_FIXED_ONE);
+    f.fix[3] = (long long)roundf(fn[0] * VCT_FIXED_ONE);
+    f.fix[4] = (long long)roundf(fn[1] * VCT_FIXED_ONE);
+    f.fix[5] = (long long)roundf(fn[2] * VCT_FIXED_ONE);
+    f.pad[0] = f.pad[1] = 0;
+    unsigned long long cnt = 1;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        int lo, hi;
+        cand_range(fmin3(q[0][a], q[1][a], q[2][a]), fmax3(q[0][a], q[1][a], q[2][a]), n, lo, hi);
+        g.lo[a] = lo;
+        g.ext[a] = hi >= lo ? (uint32_t)(hi - lo + 1) : 0u;
+        cnt *= g.ext[a];
+    }
+    g.pad = 0;
+    geom[t] = g;
+    fixo[t] = f;
+    counts[t] = cnt;
+    // keep the triangle for the G-buffer ray caster (world units)
+    mesh_tri[4 * t + 0] = make_float4(p[0][0], p[0][1], p[0][2], 0.0f);
+    mesh_tri[4 * t + 1] = make_float4(e1[0], e1[1], e1[2], 0.0f);
+    mesh_tri[4 * t + 2] = make_float4(e2[0], e2[1], e2[2], 0.0f);
+    mesh_tri[4 * t + 3] = make_float4(alb.x, alb.y, alb.z, 0.0f);
+}
+
+// ---- exclusive scan of per-triangle candidate counts (u64) ----------------
+constexpr int kScanBlock = 256, kScanItems = 4, kScanTile = kScanBlock * kScanItems;
+
+__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v,
+                                                             unsigned long long* sh,
+                                                             unsigned long long& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        unsigned long long y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    unsigned long long base = 0;
+    for (int w = 0; w < wid; ++w) base += sh[w];
+    total = sh[0] + sh[1] + sh[2] + sh[3];
+    __syncthreads();
+    return base + x - v;
+}
+
+__global__ void __launch_bounds__(kScanBlock) k_scan_tiles(const unsigned long long* __restrict__ in,
+                                                           unsigned long long* __restrict__ out,
+                                                           unsigned long long* __restrict__ tile_sums,
+                                                           uint32_t count) {
+    __shared__ unsigned long long sh[4];
+    const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
+    unsigned long long v[kScanItems], s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        v[i] = base + i < count ? in[base + i] : 0ull;
+        s += v[i];
+    }
+    unsigned long long total;
+    unsigned long long ex = block_excl_scan(s, sh, total);
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        if (base + i < count) out[base + i] = ex;
+        ex += v[i];
+    }
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
+}
+
+// single-block carry scan over the tile sums (n_tiles small: n_tri / 1024)
+__global__ void __launch_bounds__(kScanBlock) k_scan_carry(unsigned long long* __restrict__ tile_sums,
+                                                           uint32_t n_tiles,
+                                                           unsigned long long* __restrict__ total_out) {
+    __shared__ unsigned long long sh[4];
+    unsigned long long carry = 0;
+    for (uint32_t b = 0; b < n_tiles; b += kScanBlock) {
+        uint32_t i = b + threadIdx.x;
+        unsigned long long v = i < n_tiles ? tile_sums[i] : 0ull, tot;
+        unsigned long long ex = block_excl_scan(v, sh, tot);
+        if (i < n_tiles) tile_sums[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *total_out = carry;
+}
+
+__global__ void __launch_bounds__(kScanBlock) k_scan_add(unsigned long long* __restrict__ out,
+                                                         const unsigned long long* __restrict__ tile_sums,
+                                                         uint32_t count) {
+    const size_t base = (size_t)blockIdx.x * kScanTile;
+    const unsigned long long add = tile_sums[blockIdx.x];
+    for (int i = threadIdx.x; i < kScanTile; i += kScanBlock)
+        if (base + i < count) out[base + i] += add;
+}
+
+// ---- exact 13-axis triangle/voxel SAT (same rule as oracle/vct_oracle.c) --
+__device__ __forceinline__ bool tri_box_overlap(const float* __restrict__ q, float cx, float cy, float cz) {
+    float a0x = q[0] - cx, a0y = q[1] - cy, a0z = q[2] - cz;
+    float a1x = q[3] - cx, a1y = q[4] - cy, a1z = q[5] - cz;
+    float a2x = q[6] - cx, a2y = q[7] - cy, a2z = q[8] - cz;
+    if (fmin3(a0x, a1x, a2x) > 0.5f || fmax3(a0x, a1x, a2x) < -0.5f) return false;
+    if (fmin3(a0y, a1y, a2y) > 0.5f || fmax3(a0y, a1y, a2y) < -0.5f) return false;
+    if (fmin3(a0z, a1z, a2z) > 0.5f || fmax3(a0z, a1z, a2z) < -0.5f) return false;
+    float e[3][3] = {{a1x - a0x, a1y - a0y, a1z - a0z},
+                     {a2x - a1x, a2y - a1y, a2z - a1z},
+                     {a0x - a2x, a0y - a2y, a0z - a2z}};
+    {
+        float nx = e[0][1] * e[1][2] - e[0][2] * e[1][1];
+        float ny = e[0][2] * e[1][0] - e[0][0] * e[1][2];
+        float nz = e[0][0] * e[1][1] - e[0][1] * e[1][0];
+        float vminx, vmaxx, vminy, vmaxy, vminz, vmaxz;
+        if (nx > 0.0f) { vminx = -0.5f - a0x; vmaxx = 0.5f - a0x; } else { vminx = 0.5f - a0x; vmaxx = -0.5f - a0x; }
+        if (ny > 0.0f) { vminy = -0.5f - a0y; vmaxy = 0.5f - a0y; } else { vminy = 0.5f - a0y; vmaxy = -0.5f - a0y; }
+        if (nz > 0.0f) { vminz = -0.5f - a0z; vmaxz = 0.5f - a0z; } else { vminz = 0.5f - a0z; vmaxz = -0.5f - a0z; }
+        if (dot3(nx, ny, nz, vminx, vminy, vminz) > 0.0f) return false;
+        if (!(dot3(nx, ny, nz, vmaxx, vmaxy, vmaxz) >= 0.0f)) return false;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float ex = e[i][0], ey = e[i][1], ez = e[i][2];
+        const float ax[3][3] = {{0.0f, -ez, ey}, {ez, 0.0f, -ex}, {-ey, ex, 0.0f}};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float ux = ax[j][0], uy = ax[j][1], uz = ax[j][2];
+            float p0 = dot3(ux, uy, uz, a0x, a0y, a0z);
+            float p1 = dot3(ux, uy, uz, a1x, a1y, a1z);
+            float p2 = dot3(ux, uy, uz, a2x, a2y, a2z);
+            float rad = 0.5f * ((fabsf(ux) + fabsf(uy)) + fabsf(uz));
+            if (fmin3(p0, p1, p2) > rad || fmax3(p0, p1, p2) < -rad) return false;
+        }
+    }
+    return true;
+}
+
+constexpr int kCandPerThread = 8;
+
+// one lane = kCandPerThread consecutive (triangle, voxel) candidates
+__global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__ geom,
+                                                     const TriFix* __restrict__ fixr,
+                                                     const unsigned long long* __restrict__ offs,
+                                                     uint32_t n_tri, const unsigned long long* __restrict__ total_p,
+                                                     int n, long long* __restrict__ accum) {
+    const unsigned long long total = *total_p;
+    const unsigned long long c0 = ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x) * kCandPerThread;
+    if (c0 >= total) return;
+    // upper_bound(offs, c0) - 1
+    uint32_t lo = 0, hi = n_tri;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (offs[mid] <= c0) lo = mid; else hi = mid;
+    }
+    uint32_t t = lo;
+    while (t + 1 < n_tri && offs[t + 1] <= c0) ++t;  // skip zero-count triangles
+    unsigned long long next = t + 1 < n_tri ? offs[t + 1] : total;
+    for (int k = 0; k < kCandPerThread; ++k) {
+        const unsigned long long c = c0 + k;
+        if (c >= total) break;
+        while (c >= next) { ++t; next = t + 1 < n_tri ? offs[t + 1] : total; }
+        const TriGeom& g = geom[t];
+        unsigned long long local = c - offs[t];
+        uint32_t ex = g.ext[0], ey = g.ext[1];
+        uint32_t x = (uint32_t)(local % ex);
+        unsigned long long r = local / ex;
+        uint32_t y = (uint32_t)(r % ey);
+        uint32_t z = (uint32_t)(r / ey);
+        int vx = g.lo[0] + (int)x, vy = g.lo[1] + (int)y, vz = g.lo[2] + (int)z;
+        float q[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) q[i] = g.q[i];
+        if (!tri_box_overlap(q, (float)vx + 0.5f, (float)vy + 0.5f, (float)vz + 0.5f)) continue;
+        size_t v = (size_t)vx + (size_t)n * ((size_t)vy + (size_t)n * (size_t)vz);
+        unsigned long long* a = (unsigned long long*)(accum + 8 * v);
+        const TriFix& f = fixr[t];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) atomicAdd(a + i, (unsigned long long)f.fix[i]);
+        atomicAdd(a + 6, 1ull);
+    }
+}
+
+// K1 resolve: accumulators -> albedo/occupancy, normal, occupancy bitmask
+__global__ void __launch_bounds__(256) k1_resolve(const long long* __restrict__ accum, size_t nv,
+                                                  float4* __restrict__ albedo_occ,
+                                                  float4* __restrict__ normal,
+                                                  unsigned long long* __restrict__ occ_bits) {
+    size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool in = v < nv;
+    long long s[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (in) {
+        const longlong2* a = (const longlong2*)(accum + 8 * v);
+        longlong2 p0 = a[0], p1 = a[1], p2 = a[2], p3 = a[3];
+        s[0] = p0.x; s[1] = p0.y; s[2] = p1.x; s[3] = p1.y; s[4] = p2.x; s[5] = p2.y; s[6] = p3.x;
+    }
+    const unsigned long long cnt = (unsigned long long)s[6];
+    unsigned long long mask = __ballot(in && cnt > 0);
+    if (in && (threadIdx.x & 63) == 0) occ_bits[v >> 6] = mask;
+    if (!in) return;
+    if (cnt == 0) {
+        albedo_occ[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        normal[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        return;
+    }
+    double den = (double)cnt * VCT_FIXED_ONE_D;
+    float4 ao = make_float4((float)((double)s[0] / den), (float)((double)s[1] / den),
+                            (float)((double)s[2] / den), 1.0f);
+    double sx = (double)s[3], sy = (double)s[4], sz = (double)s[5];
+    double len = sqrt((sx * sx + sy * sy) + sz * sz);
+    float4 nm = len > 0.0 ? make_float4((float)(sx / len), (float)(sy / len), (float)(sz / len), 0.0f)
+                          : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    albedo_occ[v] = ao;
+    normal[v] = nm;
+}
+
+// ---- K2 injection ----------------------------------------------------------
+__device__ __forceinline__ bool occ_at(const unsigned long long* __restrict__ bits, int n, int x, int y, int z) {
+    size_t v = (size_t)x + (size_t)n * ((size_t)y + (size_t)n * (size_t)z);
+    return (bits[v >> 6] >> (v & 63)) & 1ull;
+}
+
+__device__ float dda_visibility(const unsigned long long* __restrict__ bits, int N, float qx, float qy,
+                                float qz, float lx, float ly, float lz) {
+    int vx = (int)floorf(qx), vy = (int)floorf(qy), vz = (int)floorf(qz);
+    if (vx < 0 || vy < 0 || vz < 0 || vx >= N || vy >= N || vz >= N) return 1.0f;
+    int sx = lx > 0.0f ? 1 : (lx < 0.0f ? -1 : 0);
+    int sy = ly > 0.0f ? 1 : (ly < 0.0f ? -1 : 0);
+    int sz = lz > 0.0f ? 1 : (lz < 0.0f ? -1 : 0);
+    const float inf = __builtin_inff();
+    float tdx = sx ? 1.0f / fabsf(lx) : inf;
+    float tdy = sy ? 1.0f / fabsf(ly) : inf;
+    float tdz = sz ? 1.0f / fabsf(lz) : inf;
+    float tmx = sx > 0 ? ((float)(vx + 1) - qx) * tdx : (sx < 0 ? (qx - (float)vx) * tdx : inf);
+    float tmy = sy > 0 ? ((float)(vy + 1) - qy) * tdy : (sy < 0 ? (qy - (float)vy) * tdy : inf);
+    float tmz = sz > 0 ? ((float)(vz + 1) - qz) * tdz : (sz < 0 ? (qz - (float)vz) * tdz : inf);
+    for (;;) {
+        if (occ_at(bits, N, vx, vy, vz)) return 0.0f;
+        if (tmx <= tmy && tmx <= tmz) {
+            vx += sx; if (vx < 0 || vx >= N) return 1.0f; tmx = tmx + tdx;
+        } else if (tmy <= tmz) {
+            vy += sy; if (vy < 0 || vy >= N) return 1.0f; tmy = tmy + tdy;
+        } else {
+            vz += sz; if (vz < 0 || vz >= N) return 1.0f; tmz = tmz + tdz;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k2_inject(const float4* __restrict__ albedo_occ,
+                                                 const float4* __restrict__ normal,
+                                                 const unsigned long long* __restrict__ bits, int n,
+                                                 float lx, float ly, float lz, float cr, float cg,
+                                                 float cb, float4* __restrict__ r0) {
+    size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t nv = (size_t)n * n * n;
+    if (v >= nv) return;
+    float4 ao = albedo_occ[v];
+    if (ao.w == 0.0f) { r0[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f); return; }
+    float4 nm = normal[v];
+    float ndl = dot3(nm.x, nm.y, nm.z, lx, ly, lz);
+    float4 out = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+    if (ndl > 0.0f) {
+        int x = (int)(v % n), y = (int)((v / n) % n), z = (int)(v / ((size_t)n * n));
+        float vis = dda_visibility(bits, n, ((float)x + 0.5f) + nm.x, ((float)y + 0.5f) + nm.y,
+                                   ((float)z + 0.5f) + nm.z, lx, ly, lz);
+        out.x = ((ao.x * cr) * ndl) * vis;
+        out.y = ((ao.y * cg) * ndl) * vis;
+        out.z = ((ao.z * cb) * ndl) * vis;
+    }
+    r0[v] = out;
+}
+
+}  // namespace
+
+hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
+                           uint32_t n_verts, const uint32_t* d_idx, uint32_t n_tri, const uint32_t* d_mat,
+                           const float4* d_kd, uint32_t n_mat, int* d_err) {
+    Grid& g = c->grid;
+    hipStream_t s = c->stream;
+    const size_t nv = (size_t)g.n * g.n * g.n;
+    hipError_t e;
+    // scratch layout: geom | fix | counts | offsets | tile sums | total
+    const uint32_t n_tiles = (n_tri + kScanTile - 1) / kScanTile;
+    size_t off_geom = 0;
+    size_t off_fix = off_geom + sizeof(TriGeom) * (size_t)n_tri;
+    size_t off_cnt = off_fix + sizeof(TriFix) * (size_t)n_tri;
+    size_t off_offs = off_cnt + 8 * (size_t)n_tri;
+    size_t off_tiles = off_offs + 8 * (size_t)n_tri;
+    size_t off_total = off_tiles + 8 * (size_t)(n_tiles + 1);
+    size_t bytes = off_total + 64;
+    void* sp;
+    if ((e = scratch_get(c, 1, bytes, &sp)) != hipSuccess) return e;
+    char* base = (char*)sp;
+    TriGeom* geom = (TriGeom*)(base + off_geom);
+    TriFix* fix = (TriFix*)(base + off_fix);
+    unsigned long long* cnt = (unsigned long long*)(base + off_cnt);
+    unsigned long long* offs = (unsigned long long*)(base + off_offs);
+    unsigned long long* tiles = (unsigned long long*)(base + off_tiles);
+    unsigned long long* total = (unsigned long long*)(base + off_total);
+
+    if ((e = hipMemsetAsync(g.accum, 0, nv * 64, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(total, 0, 8, s)) != hipSuccess) return e;
+    if (n_tri > 0) {
+        hipLaunchKernelGGL(k1_tri_setup, dim3((n_tri + 255) / 256), dim3(256), 0, s,
+                           (const char*)d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat,
+                           (int)g.n, g.g0[0], g.g0[1], g.g0[2], g.inv_h, geom, fix, cnt,
+                           c->mesh.tri, d_err);
+        hipLaunchKernelGGL(k_scan_tiles, dim3(n_tiles), dim3(kScanBlock), 0, s, cnt, offs, tiles, n_tri);
+        hipLaunchKernelGGL(k_scan_carry, dim3(1), dim3(kScanBlock), 0, s, tiles, n_tiles, total);
+        hipLaunchKernelGGL(k_scan_add, dim3(n_tiles), dim3(kScanBlock), 0, s, offs, tiles, n_tri);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        // the candidate total is only known on the device: read it back to size the grid
+        unsigned long long h_total = 0;
+        if ((e = hipMemcpyAsync(&h_total, total, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (h_total > 0) {
+            unsigned long long threads = (h_total + kCandPerThread - 1) / kCandPerThread;
+            unsigned long long blocks = (threads + 255) / 256;
+            if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+            hipLaunchKernelGGL(k1_candidates, dim3((uint32_t)blocks), dim3(256), 0, s, geom, fix, offs,
+                               n_tri, total, (int)g.n, g.accum);
+        }
+    }
+    hipLaunchKernelGGL(k1_resolve, dim3((uint32_t)((nv + 255) / 256)), dim3(256), 0, s, g.accum, nv,
+                       g.albedo_occ, g.normal, g.occ_bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb) {
+    Grid& g = c->grid;
+    const size_t nv = (size_t)g.n * g.n * g.n;
+    hipLaunchKernelGGL(k2_inject, dim3((uint32_t)((nv + 255) / 256)), dim3(256), 0, c->stream,
+                       g.albedo_occ, g.normal, g.occ_bits, (int)g.n, lx, ly, lz, cr, cg, cb, g.pyr);
+    return hipGetLastError();
+}
+
+}  // namespace vct

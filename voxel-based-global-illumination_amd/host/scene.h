@@ -1,0 +1,57 @@
+// scene.h — host-side scene format of the reference, feeding K1 (voxelization).
+//
+// Mirrors include/stdafx.h:36-42 (`struct Vertex`: Position, Normal,
+// TexCoords, Tangent, Bitangent = 56 bytes, attribute offsets as
+// mesh.cpp:43-55), scene/material.h:5-18 (`Material` with Ka/Kd/Ks) and the
+// Mesh/Model split of scene/mesh.h:7-26, model.h:8-42.  The reference loads
+// models with assimp (model.cpp:21-148); assimp is not available on Linux in
+// this image (its vendored lib is an MSVC import library), so Model::LoadObj is
+// a small Wavefront OBJ/MTL reader covering what the VCT path consumes
+// (positions, normals, texcoords, faces triangulated as a fan, usemtl/Kd).
+#pragma once
+#include <array>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace vcthost {
+
+struct Vertex {                    // 56 bytes, stdafx.h:36-42
+    float Position[3];
+    float Normal[3];
+    float TexCoords[2];
+    float Tangent[3];
+    float Bitangent[3];
+};
+static_assert(sizeof(Vertex) == 56, "reference Vertex layout");
+
+struct Material {                  // material.h:5-18 (texture lists omitted: untextured runs)
+    std::string name;
+    std::array<float, 4> Ka{0, 0, 0, 1};
+    std::array<float, 4> Kd{1, 1, 1, 1};
+    std::array<float, 4> Ks{0, 0, 0, 1};
+};
+
+struct Mesh {                      // mesh.h:7-26 CPU copies (vertices, indices, material)
+    std::vector<Vertex> vertices;
+    std::vector<unsigned> indices;
+    int material = 0;
+};
+
+class Model {                      // model.h:8-42
+public:
+    std::vector<Mesh> meshes;
+    std::vector<Material> materials;
+
+    // Wavefront OBJ (+ mtllib).  Returns false and fills `err` on failure.
+    bool LoadObj(const std::string& path, std::string* err);
+
+    // Apply a 4x4 column-major model matrix (r_voxelization.cpp:26-29 style).
+    void Transform(const float m[16]);
+
+    // Flatten to the C-ABI arrays: vertices, indices, per-triangle material, Kd table.
+    void Flatten(std::vector<Vertex>& v, std::vector<unsigned>& idx, std::vector<unsigned>& tri_mat,
+                 std::vector<float>& kd4) const;
+};
+
+}  // namespace vcthost

@@ -1,0 +1,123 @@
+"""ctypes binding of include/vct.h (the C-ABI of the HIP path).
+
+This module only loads the in-tree ``libvct_hip.so`` built by
+``voxel-based-global-illumination_amd/Makefile``.  There is deliberately no
+CPU fallback: if the library (or a HIP device) is missing, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvct_hip.so")
+
+# every symbol include/vct.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "vct_create", "vct_destroy", "vct_last_error", "vct_status_string", "vct_abi_version",
+    "vct_get_config", "vct_set_stream", "vct_synchronize", "vct_voxelize",
+    "vct_inject_directional", "vct_build_mips", "vct_trace", "vct_trace_device",
+    "vct_tiles_for_rank", "vct_untile_device", "vct_gbuffer_raycast_device",
+    "vct_num_levels", "vct_level_dims", "vct_download_level", "vct_upload_level0",
+    "vct_level0_device", "vct_copy_level0_to_device", "vct_set_level0_from_device",
+    "vct_download_voxels", "vct_download_accum", "vct_device_alloc", "vct_device_free", "vct_memcpy",
+)
+
+STATUS = {0: "VCT_OK", 1: "VCT_EINVAL", 2: "VCT_ENOMEM", 3: "VCT_EDEVICE", 4: "VCT_ECOMM", 5: "VCT_ESTATE"}
+
+
+class VctConfig(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32),
+        ("aabb_min", C.c_float * 3),
+        ("extent", C.c_float),
+        ("aniso", C.c_uint32),
+        ("n_diffuse", C.c_uint32),
+        ("specular", C.c_uint32),
+        ("device", C.c_int32),
+    ]
+
+
+class VctCamera(C.Structure):
+    _fields_ = [
+        ("position", C.c_float * 3),
+        ("front", C.c_float * 3),
+        ("up", C.c_float * 3),
+        ("right", C.c_float * 3),
+        ("zoom_deg", C.c_float),
+        ("near_plane", C.c_float),
+        ("far_plane", C.c_float),
+    ]
+
+
+class VctTraceArgs(C.Structure):
+    _fields_ = [
+        ("pos4", C.c_void_p),
+        ("nrm4", C.c_void_p),
+        ("alb4", C.c_void_p),
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("eye", C.c_float * 3),
+        ("diffuse4", C.c_void_p),
+        ("spec4", C.c_void_p),
+        ("steps_px", C.c_void_p),
+        ("cone_steps", C.c_void_p),
+        ("texel_fetches", C.c_void_p),
+        ("tile_rank", C.c_uint32),
+        ("tile_world", C.c_uint32),
+        ("tile_compact", C.c_uint32),
+        ("variant", C.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libvct_hip.so once; raises FileNotFoundError if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(
+            f"{LIB_PATH} is missing: build it with `make -C voxel-based-global-illumination_amd` "
+            "(the VCT path has no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    u32, i32, f32 = C.c_uint32, C.c_int32, C.c_float
+    sig = {
+        "vct_create": (i32, [C.POINTER(VctConfig), C.POINTER(P)]),
+        "vct_destroy": (None, [P]),
+        "vct_last_error": (C.c_char_p, [P]),
+        "vct_status_string": (C.c_char_p, [i32]),
+        "vct_abi_version": (u32, []),
+        "vct_get_config": (i32, [P, C.POINTER(VctConfig)]),
+        "vct_set_stream": (i32, [P, P]),
+        "vct_synchronize": (i32, [P]),
+        "vct_voxelize": (i32, [P, P, u32, u32, P, u32, P, P, u32]),
+        "vct_inject_directional": (i32, [P, C.POINTER(f32), C.POINTER(f32)]),
+        "vct_build_mips": (i32, [P]),
+        "vct_trace": (i32, [P, P, P, P, u32, u32, C.POINTER(f32), P, P, P, P]),
+        "vct_trace_device": (i32, [P, C.POINTER(VctTraceArgs)]),
+        "vct_tiles_for_rank": (u32, [u32, u32, u32, u32]),
+        "vct_untile_device": (i32, [P, P, u32, u32, u32, P]),
+        "vct_gbuffer_raycast_device": (i32, [P, C.POINTER(VctCamera), u32, u32, f32, P, P, P]),
+        "vct_num_levels": (u32, [P]),
+        "vct_level_dims": (i32, [P, u32, C.POINTER(u32), C.POINTER(u32)]),
+        "vct_download_level": (i32, [P, u32, u32, P]),
+        "vct_upload_level0": (i32, [P, P]),
+        "vct_level0_device": (i32, [P, C.POINTER(P), C.POINTER(C.c_size_t)]),
+        "vct_copy_level0_to_device": (i32, [P, P]),
+        "vct_set_level0_from_device": (i32, [P, P]),
+        "vct_download_voxels": (i32, [P, P, P]),
+        "vct_download_accum": (i32, [P, P, P]),
+        "vct_device_alloc": (i32, [P, C.c_size_t, C.POINTER(P)]),
+        "vct_device_free": (i32, [P, P]),
+        "vct_memcpy": (i32, [P, P, P, C.c_size_t, C.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,248 @@
+"""Synthetic scenes and G-buffers.
+
+Sponza, San Miguel and the reference's nanosuit.obj are not available offline
+(SURVEY.md 0, 8c), so the configs run on procedural stand-ins at the same grid
+and framebuffer sizes:
+
+* ``cornell()``: the unit Cornell box [-1,1]^3 without its front face, red left
+  wall, green right wall, a short and a tall box; the ceiling has a skylight
+  opening so the canonical directional light normalize(0.3, 1, 0.2) reaches the
+  interior (with a closed ceiling every voxel would be in shadow);
+* ``atrium()``: the "Sponza-class" stand-in: an atrium with a long roof
+  opening, two colonnades of four columns, two gallery slabs, coloured walls;
+* ``random_triangles()``: a triangle soup for voxelization stress / parity.
+
+Geometry is emitted in the reference ``Vertex`` layout (include/stdafx.h:36-42:
+Position, Normal, TexCoords, Tangent, Bitangent = 14 floats = 56 bytes,
+attribute offsets as mesh.cpp:43-55), uint32 triangle indices, a per-triangle
+material index and a Kd table (scene/material.h:10).
+
+G-buffers: ``G_scene`` comes from the HIP ray caster (vct_gbuffer_raycast_device)
+or, for small CPU-side fixtures, :func:`raycast_numpy`; ``G_rand`` is
+:func:`gbuffer_rand` (positions on occupied voxel centres, jittered voxel
+normals, roughness U[0.05, 0.3]; seed 42).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import VERTEX_FLOATS
+
+LIGHT_DIR = (0.3, 1.0, 0.2)      # dir_to_light, SURVEY 8d (normalised by vct_inject_directional)
+LIGHT_COLOR = (1.0, 1.0, 1.0)
+ROUGHNESS = 0.1                  # G_scene roughness everywhere
+
+
+def grid_for_unit_box(n: int):
+    """Grid AABB = [-1,1]^3 padded by one voxel: E = 2n/(n-2), centred on 0."""
+    extent = 2.0 * n / (n - 2)
+    return (-extent / 2, -extent / 2, -extent / 2), extent
+
+
+@dataclass
+class Scene:
+    name: str
+    verts: list = field(default_factory=list)   # rows of 14 floats
+    idx: list = field(default_factory=list)
+    tri_mat: list = field(default_factory=list)
+    kd: list = field(default_factory=list)      # rgba rows
+
+    def material(self, rgb) -> int:
+        self.kd.append((float(rgb[0]), float(rgb[1]), float(rgb[2]), 1.0))
+        return len(self.kd) - 1
+
+    def tri(self, p0, p1, p2, mat: int):
+        p0, p1, p2 = (np.asarray(p, np.float64) for p in (p0, p1, p2))
+        n = np.cross(p1 - p0, p2 - p0)
+        ln = np.linalg.norm(n)
+        n = n / ln if ln > 0 else n
+        base = len(self.verts)
+        for p in (p0, p1, p2):
+            self.verts.append([p[0], p[1], p[2], n[0], n[1], n[2]] + [0.0] * (VERTEX_FLOATS - 6))
+        self.idx += [base, base + 1, base + 2]
+        self.tri_mat.append(mat)
+
+    def quad(self, p0, p1, p2, p3, normal, mat: int):
+        """Quad p0..p3 (in order around the edge) whose face normal points along `normal`."""
+        p0, p1, p2, p3 = (np.asarray(p, np.float64) for p in (p0, p1, p2, p3))
+        if np.dot(np.cross(p1 - p0, p2 - p0), normal) < 0:
+            p1, p3 = p3, p1
+        self.tri(p0, p1, p2, mat)
+        self.tri(p0, p2, p3, mat)
+
+    def box(self, lo, hi, mat: int):
+        """Axis-aligned box with outward normals."""
+        x0, y0, z0 = lo
+        x1, y1, z1 = hi
+        self.quad((x0, y0, z0), (x0, y1, z0), (x0, y1, z1), (x0, y0, z1), (-1, 0, 0), mat)
+        self.quad((x1, y0, z0), (x1, y1, z0), (x1, y1, z1), (x1, y0, z1), (1, 0, 0), mat)
+        self.quad((x0, y0, z0), (x1, y0, z0), (x1, y0, z1), (x0, y0, z1), (0, -1, 0), mat)
+        self.quad((x0, y1, z0), (x1, y1, z0), (x1, y1, z1), (x0, y1, z1), (0, 1, 0), mat)
+        self.quad((x0, y0, z0), (x1, y0, z0), (x1, y1, z0), (x0, y1, z0), (0, 0, -1), mat)
+        self.quad((x0, y0, z1), (x1, y0, z1), (x1, y1, z1), (x0, y1, z1), (0, 0, 1), mat)
+
+    def rect_y(self, y, x0, x1, z0, z1, ny, mat):
+        self.quad((x0, y, z0), (x1, y, z0), (x1, y, z1), (x0, y, z1), (0, ny, 0), mat)
+
+    def arrays(self):
+        """(verts (V,14) f32, idx (3T,) u32, tri_mat (T,) u32, kd (M,4) f32)"""
+        return (np.asarray(self.verts, np.float32).reshape(-1, VERTEX_FLOATS),
+                np.asarray(self.idx, np.uint32),
+                np.asarray(self.tri_mat, np.uint32),
+                np.asarray(self.kd, np.float32).reshape(-1, 4))
+
+    @property
+    def n_tri(self):
+        return len(self.tri_mat)
+
+
+def _ceiling_with_hole(s: Scene, hx0, hx1, hz0, hz1, mat):
+    """Ceiling y = 1 (normal -y) with a rectangular skylight [hx0,hx1] x [hz0,hz1]."""
+    s.rect_y(1.0, -1.0, 1.0, -1.0, hz0, -1, mat)
+    s.rect_y(1.0, -1.0, 1.0, hz1, 1.0, -1, mat)
+    s.rect_y(1.0, -1.0, hx0, hz0, hz1, -1, mat)
+    s.rect_y(1.0, hx1, 1.0, hz0, hz1, -1, mat)
+
+
+def cornell() -> Scene:
+    s = Scene("cornell")
+    white = s.material((0.725, 0.71, 0.68))
+    red = s.material((0.63, 0.065, 0.05))
+    green = s.material((0.14, 0.45, 0.091))
+    s.rect_y(-1.0, -1.0, 1.0, -1.0, 1.0, 1, white)                                   # floor
+    _ceiling_with_hole(s, -0.5, 0.5, -0.5, 0.5, white)                               # ceiling
+    s.quad((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1), (0, 0, 1), white)     # back
+    s.quad((-1, -1, -1), (-1, 1, -1), (-1, 1, 1), (-1, -1, 1), (1, 0, 0), red)       # left
+    s.quad((1, -1, -1), (1, 1, -1), (1, 1, 1), (1, -1, 1), (-1, 0, 0), green)        # right
+    s.box((0.05, -1.0, 0.0), (0.65, -0.4, 0.6), white)                               # short box
+    s.box((-0.65, -1.0, -0.6), (-0.05, 0.2, 0.0), white)                             # tall box
+    return s
+
+
+def atrium() -> Scene:
+    """Sponza-class stand-in: atrium with colonnades, galleries and a roof opening."""
+    s = Scene("atrium")
+    stone = s.material((0.72, 0.68, 0.60))
+    floor = s.material((0.55, 0.50, 0.45))
+    red = s.material((0.60, 0.12, 0.10))
+    blue = s.material((0.12, 0.20, 0.55))
+    green = s.material((0.20, 0.45, 0.15))
+    ochre = s.material((0.75, 0.55, 0.20))
+    s.rect_y(-1.0, -1.0, 1.0, -1.0, 1.0, 1, floor)
+    _ceiling_with_hole(s, -0.35, 0.35, -0.85, 0.85, stone)
+    s.quad((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1), (0, 0, 1), ochre)
+    s.quad((-1, -1, -1), (-1, 1, -1), (-1, 1, 1), (-1, -1, 1), (1, 0, 0), red)
+    s.quad((1, -1, -1), (1, 1, -1), (1, 1, 1), (1, -1, 1), (-1, 0, 0), blue)
+    # two gallery slabs along the side walls at mid height
+    s.box((-1.0, 0.05, -1.0), (-0.55, 0.15, 0.8), stone)
+    s.box((0.55, 0.05, -1.0), (1.0, 0.15, 0.8), stone)
+    # colonnades: 4 columns per side (ground floor) + 4 per side (gallery level)
+    for side in (-1, 1):
+        x = side * 0.5
+        for k in range(4):
+            z = -0.8 + k * 0.5
+            s.box((x - 0.06, -1.0, z - 0.06), (x + 0.06, 0.05, z + 0.06), stone)
+            s.box((x - 0.045, 0.15, z - 0.045), (x + 0.045, 0.85, z + 0.045), stone)
+        # balustrade on the gallery edge
+        s.box((x - 0.03, 0.15, -0.95), (x + 0.03, 0.3, 0.75), green)
+    # a fountain block in the middle of the court
+    s.box((-0.2, -1.0, -0.2), (0.2, -0.8, 0.2), stone)
+    return s
+
+
+def random_triangles(n_tri: int, seed: int = 7, size: float = 0.3) -> Scene:
+    """Triangle soup inside [-1,1]^3 (sizes up to `size`), random materials."""
+    rng = np.random.default_rng(seed)
+    s = Scene("random")
+    mats = [s.material(rng.uniform(0.05, 0.95, 3)) for _ in range(5)]
+    c = rng.uniform(-0.9, 0.9, (n_tri, 3))
+    for t in range(n_tri):
+        p = c[t] + rng.uniform(-size, size, (3, 3))
+        s.tri(p[0], p[1], p[2], mats[t % len(mats)])
+    return s
+
+
+SCENES = {"cornell": cornell, "atrium": atrium}
+
+
+# ---------------------------------------------------------------------------
+# G-buffers
+# ---------------------------------------------------------------------------
+
+def raycast_numpy(scene: Scene, cam, w: int, h: int, roughness: float = ROUGHNESS):
+    """CPU G_scene (same ray rule as the HIP caster; for small fixtures only)."""
+    verts, idx, mat, kd = scene.arrays()
+    P = verts[:, :3].astype(np.float64)[idx.reshape(-1, 3)]
+    v0, e1, e2 = P[:, 0], P[:, 1] - P[:, 0], P[:, 2] - P[:, 0]
+    th = np.tan(np.radians(cam.zoom) / 2)
+    aspect = w / h
+    xs = (2 * (np.arange(w) + 0.5) / w - 1) * th * aspect
+    ys = (1 - 2 * (np.arange(h) + 0.5) / h) * th
+    X, Y = np.meshgrid(xs, ys)
+    d = cam.front[None, None] + X[..., None] * cam.right + Y[..., None] * cam.up
+    d /= np.linalg.norm(d, axis=-1, keepdims=True)
+    d = d.reshape(-1, 3)
+    o = cam.position
+    best = np.full(d.shape[0], np.inf)
+    hit = np.full(d.shape[0], -1)
+    for t in range(len(v0)):
+        pv = np.cross(d, e2[t])
+        det = pv @ e1[t]
+        ok = np.abs(det) >= 1e-12
+        inv = np.where(ok, 1.0 / np.where(ok, det, 1.0), 0.0)
+        tv = o - v0[t]
+        u = (pv @ tv) * inv
+        qv = np.cross(tv, e1[t])
+        v = (d @ qv) * inv
+        tt = (qv @ e2[t]) * inv
+        m = ok & (u >= 0) & (u <= 1) & (v >= 0) & (u + v <= 1) & (tt > 0) & (tt < best)
+        best[m] = tt[m]
+        hit[m] = t
+    depth = best * (d @ cam.front)
+    valid = (hit >= 0) & (depth >= cam.near) & (depth <= cam.far)
+    pos = np.zeros((d.shape[0], 4), np.float32)
+    nrm = np.zeros((d.shape[0], 4), np.float32)
+    alb = np.zeros((d.shape[0], 4), np.float32)
+    alb[:, 3] = roughness
+    hv = hit[valid]
+    pos[valid, :3] = o + d[valid] * best[valid, None]
+    pos[valid, 3] = 1.0
+    fn = np.cross(e1[hv], e2[hv])
+    fn /= np.linalg.norm(fn, axis=-1, keepdims=True)
+    flip = np.einsum("ij,ij->i", fn, d[valid]) > 0
+    fn[flip] *= -1
+    nrm[valid, :3] = fn
+    alb[valid, :3] = kd[mat[hv], :3]
+    return pos.reshape(h, w, 4), nrm.reshape(h, w, 4), alb.reshape(h, w, 4)
+
+
+def gbuffer_rand(albedo_occ: np.ndarray, normal: np.ndarray, aabb_min, extent: float, w: int, h: int,
+                 seed: int = 42):
+    """G_rand: cache-hostile stress G-buffer on occupied voxel centres."""
+    n = albedo_occ.shape[0]
+    rng = np.random.default_rng(seed)
+    flat_occ = albedo_occ.reshape(-1, 4)[:, 3] > 0
+    occ = np.flatnonzero(flat_occ)
+    if occ.size == 0:
+        raise ValueError("empty voxel grid")
+    pick = occ[rng.integers(0, occ.size, w * h)]
+    x, y, z = pick % n, (pick // n) % n, pick // (n * n)
+    hvox = extent / n
+    g0 = np.asarray(aabb_min, np.float64)
+    pos = np.ones((w * h, 4), np.float32)
+    pos[:, 0] = g0[0] + hvox * (x + 0.5)
+    pos[:, 1] = g0[1] + hvox * (y + 0.5)
+    pos[:, 2] = g0[2] + hvox * (z + 0.5)
+    nv = normal.reshape(-1, 4)[pick, :3].astype(np.float64)
+    zero = np.linalg.norm(nv, axis=-1) < 1e-6
+    nv[zero] = rng.normal(size=(zero.sum(), 3))
+    nv += rng.uniform(-0.1, 0.1, nv.shape)
+    nv /= np.linalg.norm(nv, axis=-1, keepdims=True)
+    nrm = np.zeros((w * h, 4), np.float32)
+    nrm[:, :3] = nv
+    alb = np.zeros((w * h, 4), np.float32)
+    alb[:, :3] = albedo_occ.reshape(-1, 4)[pick, :3]
+    alb[:, 3] = rng.uniform(0.05, 0.3, w * h)
+    return pos.reshape(h, w, 4), nrm.reshape(h, w, 4), alb.reshape(h, w, 4)
