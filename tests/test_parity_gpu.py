@@ -106,6 +106,34 @@ def test_trace_parity(gpu_ready, oracle_mod, name, n, kind, aniso, nd, spec):
     ctx.close()
 
 
+@pytest.mark.parametrize("kind", ["scene", "rand"])
+def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
+    """Both K4 variants (0 = LDS-brick default, 1 = per-lane gather) equal the oracle bit for bit."""
+    import torch
+    O = oracle_mod
+    n, w, h = 64, 160, 96
+    ctx, s, arrs, (g0, E) = gpu_pipeline(n, "atrium")
+    (pos, nrm, alb), cam = _gbuf(kind, s, ctx.download_voxels(), g0, E, w, h)
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    gb = [torch.from_numpy(a).to(dev) for a in (pos, nrm, alb)]
+    ref = O.trace(n, g0, E, ctx.download_level(0), gpu_pyramid_flat(ctx), pos, nrm, alb, cam.position)
+    for variant in (0, 1):
+        d = torch.empty((h, w, 4), device=dev)
+        sp = torch.empty((h, w, 4), device=dev)
+        st = torch.zeros((h, w), dtype=torch.int32, device=dev)
+        cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+        ctx.trace_device(*gb, w, h, cam.position, d, sp, steps_px=st, cone_steps=cnt[0:1],
+                         texel_fetches=cnt[1:2], variant=variant)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), ref["diffuse"]), f"variant {variant} diffuse"
+        assert np.array_equal(sp.cpu().numpy(), ref["spec"]), f"variant {variant} spec"
+        assert np.array_equal(st.cpu().numpy().astype(np.uint32), ref["steps_px"])
+        assert int(cnt[0]) == ref["cone_steps"]
+        assert int(cnt[1]) > 24 * int(cnt[0]) // 2   # >= 1 aniso level per step on average
+    ctx.close()
+
+
 def test_trace_edge_cases(gpu_ready, oracle_mod):
     """1x1 frame, all-background frame, odd sizes not multiple of 64, empty grid."""
     from vct import Context

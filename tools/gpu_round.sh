@@ -16,4 +16,18 @@ timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py --steps $STEPS --warmup 2 ${
 brc=$?
 echo "bench rc=$brc"; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err
 if faulted gpurun_out/bench.err; then echo "GPU FAULT in bench"; exit 99; fi
-exit $brc
+if [ $brc -ne 0 ]; then exit $brc; fi
+# extra bench configurations: EXTRA="args1;args2"
+if [ -n "$EXTRA" ]; then
+  IFS=';' read -ra XS <<< "$EXTRA"
+  i=0
+  for xa in "${XS[@]}"; do
+    i=$((i+1))
+    timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py --no-cpu-baseline $xa > gpurun_out/bench_x$i.json 2> gpurun_out/bench_x$i.err
+    xrc=$?
+    echo "extra[$i] ($xa) rc=$xrc"; cat gpurun_out/bench_x$i.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['k4_kernel_ms_avg'], d['roofline']['frac'])" 2>/dev/null
+    if faulted gpurun_out/bench_x$i.err; then echo "GPU FAULT in extra bench"; exit 99; fi
+    if [ $xrc -ne 0 ]; then tail -5 gpurun_out/bench_x$i.err; exit $xrc; fi
+  done
+fi
+exit 0

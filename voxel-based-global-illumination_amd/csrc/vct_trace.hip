@@ -94,7 +94,9 @@ __device__ __forceinline__ float4 tri_gather(const float4* __restrict__ vol, con
     return acc;
 }
 
-// D_l(q, d) (A.5): level 0 isotropic, level >= 1 directional over 3 faces
+// D_l(q, d) (A.5): level 0 isotropic, level >= 1 directional over 3 faces.
+// s = fmaf(wd_z, T_z, fmaf(wd_y, T_y, wd_x * T_x)) written as a face loop that
+// starts from 0 (fmaf(w, t, 0) == w * t); one face's 8 gathers are live at a time.
 __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx, float qy, float qz,
                                                int fx, int fy, int fz, float wdx, float wdy, float wdz) {
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
@@ -104,14 +106,17 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
     const float4* lvl = k.pyr + k.lvl_off[l];
     if (l == 0 || !k.aniso) return tri_gather(lvl, t);
     const size_t vl = (size_t)nl * nl * nl;
-    float4 tx = tri_gather(lvl + (size_t)fx * vl, t);
-    float4 ty = tri_gather(lvl + (size_t)fy * vl, t);
-    float4 tz = tri_gather(lvl + (size_t)fz * vl, t);
-    float4 s;
-    s.x = fmaf(wdz, tz.x, fmaf(wdy, ty.x, wdx * tx.x));
-    s.y = fmaf(wdz, tz.y, fmaf(wdy, ty.y, wdx * tx.y));
-    s.z = fmaf(wdz, tz.z, fmaf(wdy, ty.z, wdx * tx.z));
-    s.w = fmaf(wdz, tz.w, fmaf(wdy, ty.w, wdx * tx.w));
+    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll 1
+    for (int f = 0; f < 3; ++f) {
+        const int face = f == 0 ? fx : (f == 1 ? fy : fz);
+        const float w = f == 0 ? wdx : (f == 1 ? wdy : wdz);
+        const float4 tf = tri_gather(lvl + (size_t)face * vl, t);
+        s.x = fmaf(w, tf.x, s.x);
+        s.y = fmaf(w, tf.y, s.y);
+        s.z = fmaf(w, tf.z, s.z);
+        s.w = fmaf(w, tf.w, s.w);
+    }
     return s;
 }
 
@@ -220,6 +225,275 @@ __global__ void __launch_bounds__(256) k4_trace(TraceK k) {
             float4 res;
             steps += march(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
             sout = res;
+        }
+    }
+    if (in_frame || k.compact) {
+        k.diff[oidx] = dout;
+        k.spec[oidx] = sout;
+        if (k.steps_px && in_frame) k.steps_px[pix] = steps;
+    }
+    if (k.steps_total) {
+        uint32_t ws = wave_sum_u32(steps);
+        if (lane == 0 && ws) atomicAdd(k.steps_total, (unsigned long long)ws);
+    }
+    if (k.texels_total) {
+        uint32_t wt = wave_sum_u32(texels);
+        if (lane == 0 && wt) atomicAdd(k.texels_total, (unsigned long long)wt);
+    }
+}
+
+// ===========================================================================
+// Default variant (0): wave-cooperative 4^3 brick staging in LDS
+// ===========================================================================
+// The 64 lanes of a wave (an 8x8 pixel block) march the same cone index in
+// lock step.  At each step and mip level, if every active lane's 2x2x2
+// trilinear footprint lies inside the 4^3 texel brick centred on the first
+// active lane (a ballot), the wave loads that brick ONCE -- one texel per
+// lane, one 16-B global load per face -- into a wave-private LDS slot and every
+// lane reads its 8 corners with ds_read_b128 at immediate offsets
+// (+16 B dx, +64 B dy, +256 B dz).  That replaces 8 gathers per lane and face
+// (64 address computations, 8 TA-issued 1-KiB wave loads) by one coalesced
+// load.  Texels outside the level are staged as zero, which is exactly the
+// spec's zero border.  When the footprint does not fit (silhouettes, diverging
+// specular lobes) or the lanes disagree on the mip level or face triple, the
+// wave falls back to the per-lane gathers of variant 0 for that step.  Both
+// paths read the same texels and run the same fmaf chain, so the result is
+// bit-identical to variant 0 and to the oracle.
+constexpr int kBrickSlots = 6;              // level A: 1 or 3 faces, level B: 3 faces
+
+// component-wise select: `c ? a : b` on two float4 structs lowers to scratch on gfx950
+__device__ __forceinline__ float4 sel4(bool c, float4 a, float4 b) {
+    return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+// Orders one wave's LDS writes before its (other lanes') LDS reads and vice versa:
+// the asm "memory" clobber stops the compiler moving DS ops across it (release /
+// acquire fences at wavefront scope do not order a store before a later load of
+// a different address), the lgkmcnt(0) makes the hand-off explicit in hardware.
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float4 brick_tri(const float4* __restrict__ b, float fx, float fy, float fz) {
+    const float wx[2] = {1.0f - fx, fx}, wy[2] = {1.0f - fy, fy}, wz[2] = {1.0f - fz, fz};
+    float4 v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = b[(c & 1) + 4 * ((c >> 1) & 1) + 16 * (c >> 2)];
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float w = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
+        acc.x = fmaf(w, v[c].x, acc.x);
+        acc.y = fmaf(w, v[c].y, acc.y);
+        acc.z = fmaf(w, v[c].z, acc.z);
+        acc.w = fmaf(w, v[c].w, acc.w);
+    }
+    return acc;
+}
+
+// D_l for one level; `lds` = this wave's slots for the level (nf x 64 texels).
+// Must be called in wave-uniform control flow (all 64 lanes).
+__device__ __forceinline__ float4 level_brick(const TraceK& k, int l, float qx, float qy, float qz, bool active,
+                                              int first, bool faces_uniform, int ufaces, int fx, int fy, int fz,
+                                              float wdx, float wdy, float wdz, float4* __restrict__ lds) {
+    const float scale = __uint_as_float((uint32_t)(127 - l) << 23);
+    const int nl = k.n >> l;
+    const float cx = qx * scale - 0.5f, cy = qy * scale - 0.5f, cz = qz * scale - 0.5f;
+    const float flx = floorf(cx), fly = floorf(cy), flz = floorf(cz);
+    const int ix = (int)flx, iy = (int)fly, iz = (int)flz;
+    const bool iso = (l == 0 || !k.aniso);
+    const int ox = __builtin_amdgcn_readlane(ix, first) - 1;
+    const int oy = __builtin_amdgcn_readlane(iy, first) - 1;
+    const int oz = __builtin_amdgcn_readlane(iz, first) - 1;
+    const uint32_t lx = (uint32_t)(ix - ox), ly = (uint32_t)(iy - oy), lz = (uint32_t)(iz - oz);
+    const bool fits = __all(!active || (lx <= 2u && ly <= 2u && lz <= 2u)) && (iso || faces_uniform);
+    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float4* lvl = k.pyr + k.lvl_off[l];
+    const size_t vl = (size_t)nl * nl * nl;
+    if (fits) {
+        const int lane = threadIdx.x & 63;
+        const int sx = ox + (lane & 3), sy = oy + ((lane >> 2) & 3), sz = oz + (lane >> 4);
+        const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
+        const uint32_t gi = inb ? (uint32_t)sx + (uint32_t)nl * ((uint32_t)sy + (uint32_t)nl * (uint32_t)sz) : 0u;
+        const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        auto zsel = [inb, z4](float4 v) { return sel4(inb, v, z4); };
+        if (iso) {
+            lds[lane] = zsel(lvl[gi]);
+        } else {
+            // wave-uniform face triple (lanes that trace nothing -- background pixels --
+            // still stage texels, so the faces must not come from the lane's own direction)
+            const int ux = ufaces & 7, uy = (ufaces >> 3) & 7, uz = ufaces >> 6;
+            const float4 a = lvl[(size_t)ux * vl + gi], b = lvl[(size_t)uy * vl + gi], c = lvl[(size_t)uz * vl + gi];
+            lds[lane] = zsel(a);
+            lds[64 + lane] = zsel(b);
+            lds[128 + lane] = zsel(c);
+        }
+        wave_lds_sync();
+        if (active) {
+            const uint32_t base = lx + 4u * ly + 16u * lz;
+            const float frx = cx - flx, fry = cy - fly, frz = cz - flz;
+            if (iso) {
+                s = brick_tri(lds + base, frx, fry, frz);
+            } else {
+#pragma unroll 1
+                for (int f = 0; f < 3; ++f) {
+                    const float w = f == 0 ? wdx : (f == 1 ? wdy : wdz);
+                    const float4 tf = brick_tri(lds + 64 * f + base, frx, fry, frz);
+                    s.x = fmaf(w, tf.x, s.x);
+                    s.y = fmaf(w, tf.y, s.y);
+                    s.z = fmaf(w, tf.z, s.z);
+                    s.w = fmaf(w, tf.w, s.w);
+                }
+            }
+        }
+        wave_lds_sync();
+    } else if (active) {
+        s = sample_level(k, l, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+    }
+    return s;
+}
+
+// one cone, wave-synchronous (A.6); same arithmetic as march()
+__device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, float ox, float oy, float oz,
+                                                float dx, float dy, float dz, float tau, float4& res,
+                                                uint32_t& texels, float4* __restrict__ lds) {
+    const float tau2 = 2.0f * tau;
+    const float nf = (float)k.n, Lf = (float)k.L;
+    const int fx = dx >= 0.0f ? VCT_FACE_PX : VCT_FACE_NX;
+    const int fy = dy >= 0.0f ? VCT_FACE_PY : VCT_FACE_NY;
+    const int fz = dz >= 0.0f ? VCT_FACE_PZ : VCT_FACE_NZ;
+    const float wdx = dx * dx, wdy = dy * dy, wdz = dz * dz;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f, a = 0.0f, t = 1.0f;
+    uint32_t steps = 0;
+    bool active = valid;
+    // face triple uniform over the lanes that trace this cone
+    const int fcode = fx | (fy << 3) | (fz << 6);
+    unsigned long long vm = __ballot(valid);
+    const int f0 = vm ? __builtin_amdgcn_readlane(fcode, __builtin_ctzll(vm)) : fcode;
+    const bool faces_uniform = __all(!valid || fcode == f0);
+    for (;;) {
+        const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
+        if (active) {
+            if (!(a < VCT_ALPHA_STOP)) active = false;
+            else if (!(t <= k.tmax)) active = false;
+            else if (!(qx >= 0.0f && qx <= nf && qy >= 0.0f && qy <= nf && qz >= 0.0f && qz <= nf)) active = false;
+        }
+        const unsigned long long am = __ballot(active);
+        if (am == 0ull) break;
+        const int first = __builtin_ctzll(am);
+        const float D = fmaxf(1.0f, tau2 * t);
+        float m = spec_log2(D);
+        if (m > Lf) m = Lf;
+        const int l0 = (int)m;
+        const float fr = m - (float)l0;
+        const int l0f = __builtin_amdgcn_readlane(l0, first);
+        const bool lvl_uniform = __all(!active || l0 == l0f);
+        const bool two = fr > 0.0f && l0 < k.L;
+        float4 s;
+        if (lvl_uniform) {
+            s = level_brick(k, l0f, qx, qy, qz, active, first, faces_uniform, f0, fx, fy, fz, wdx, wdy, wdz, lds);
+            if (__any(active && two)) {
+                const int l1 = l0f + 1 <= k.L ? l0f + 1 : k.L;
+                float4 s1 = level_brick(k, l1, qx, qy, qz, active && two, first, faces_uniform, f0, fx, fy, fz,
+                                        wdx, wdy, wdz, lds + 3 * 64);
+                if (active && two) {
+                    const float omf = 1.0f - fr;
+                    s.x = fmaf(fr, s1.x, omf * s.x);
+                    s.y = fmaf(fr, s1.y, omf * s.y);
+                    s.z = fmaf(fr, s1.z, omf * s.z);
+                    s.w = fmaf(fr, s1.w, omf * s.w);
+                }
+            }
+        } else if (active) {
+            s = sample_level(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+            if (two) {
+                float4 s1 = sample_level(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+                const float omf = 1.0f - fr;
+                s.x = fmaf(fr, s1.x, omf * s.x);
+                s.y = fmaf(fr, s1.y, omf * s.y);
+                s.z = fmaf(fr, s1.z, omf * s.z);
+                s.w = fmaf(fr, s1.w, omf * s.w);
+            }
+        }
+        if (active) {
+            texels += (l0 == 0 || !k.aniso) ? 8u : 24u;
+            if (two) texels += k.aniso ? 24u : 8u;
+            const float oma = 1.0f - a;
+            cr = fmaf(oma, s.x, cr);
+            cg = fmaf(oma, s.y, cg);
+            cb = fmaf(oma, s.z, cb);
+            a = fmaf(oma, s.w, a);
+            t = t + VCT_STEP_SCALE * D;
+            ++steps;
+        }
+    }
+    res = make_float4(cr, cg, cb, a);
+    return steps;
+}
+
+__global__ void __launch_bounds__(256) k4_trace_brick(TraceK k) {
+    __shared__ float4 lds_all[4][kBrickSlots * 64];
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const uint32_t xcd = b & 7, q = nb >> 3, r = nb & 7;
+    const uint32_t rb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    const uint32_t lt = rb >> 4, sub = rb & 15;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float4* lds = lds_all[wave];
+    const uint32_t px = (sub & 3) * 16 + (wave & 1) * 8 + (lane & 7);
+    const uint32_t py = (sub >> 2) * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const uint32_t tile = lt * (uint32_t)k.world + (uint32_t)k.rank;
+    const uint32_t x = (tile % (uint32_t)k.tiles_x) * VCT_TILE + px;
+    const uint32_t y = (tile / (uint32_t)k.tiles_x) * VCT_TILE + py;
+    const bool in_frame = x < (uint32_t)k.w && y < (uint32_t)k.h;
+    const size_t pix = in_frame ? (size_t)y * (size_t)k.w + x : 0;
+    const size_t oidx = k.compact ? (size_t)lt * (VCT_TILE * VCT_TILE) + py * VCT_TILE + px : pix;
+
+    float4 dout = make_float4(0.0f, 0.0f, 0.0f, 0.0f), sout = dout;
+    uint32_t steps = 0, texels = 0;
+    float4 P = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (in_frame) P = k.pos[pix];
+    const bool valid = P.w != 0.0f;
+    if (__any(valid)) {
+        float4 N4 = make_float4(0.0f, 1.0f, 0.0f, 0.0f);
+        if (valid) N4 = k.nrm[pix];
+        const float nx = N4.x, ny = N4.y, nz = N4.z;
+        const float ox = (P.x - k.g0x) * k.inv_h + nx;
+        const float oy = (P.y - k.g0y) * k.inv_h + ny;
+        const float oz = (P.z - k.g0z) * k.inv_h + nz;
+        const float sgn = copysignf(1.0f, nz);
+        const float ka = -1.0f / (sgn + nz);
+        const float kb = (nx * ny) * ka;
+        const float Tx = 1.0f + ((sgn * nx) * nx) * ka, Ty = sgn * kb, Tz = -(sgn * nx);
+        const float Bx = kb, By = sgn + (ny * ny) * ka, Bz = -ny;
+        const float(*cones)[4] = cone_table(k.nd);
+        float ir = 0.0f, ig = 0.0f, ib = 0.0f, occ = 0.0f;
+        for (int c = 0; c < k.nd; ++c) {
+            const float cn = cones[c][0], ct = cones[c][1], cb = cones[c][2], wk = cones[c][3];
+            const float dx = (cn * nx + ct * Tx) + cb * Bx;
+            const float dy = (cn * ny + ct * Ty) + cb * By;
+            const float dz = (cn * nz + ct * Tz) + cb * Bz;
+            float4 res;
+            steps += march_brick(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds);
+            ir = fmaf(wk, res.x, ir);
+            ig = fmaf(wk, res.y, ig);
+            ib = fmaf(wk, res.z, ib);
+            occ = fmaf(wk, res.w, occ);
+        }
+        dout = sel4(valid, make_float4(ir, ig, ib, 1.0f - occ), dout);
+        if (k.spec_on) {
+            float vx = k.ex - P.x, vy = k.ey - P.y, vz = k.ez - P.z;
+            float vl = sqrtf(dot3(vx, vy, vz, vx, vy, vz));
+            vl = valid ? vl : 1.0f;
+            vx = vx / vl; vy = vy / vl; vz = vz / vl;
+            const float ndv = dot3(nx, ny, nz, vx, vy, vz);
+            const float k2 = 2.0f * ndv;
+            const float rx = k2 * nx - vx, ry = k2 * ny - vy, rz = k2 * nz - vz;
+            const float rough = valid ? k.alb[pix].w : 0.1f;
+            const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
+            float4 res;
+            steps += march_brick(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds);
+            sout = sel4(valid, res, sout);
         }
     }
     if (in_frame || k.compact) {
@@ -358,7 +632,10 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.tau_d = c->cfg.n_diffuse == 16 ? VCT_TAN20 : VCT_TAN30;
     if (nlt == 0) return hipSuccess;
     const uint32_t blocks = nlt * 16;
-    hipLaunchKernelGGL(k4_trace, dim3(blocks), dim3(256), 0, c->stream, k);
+    if (a->variant == 0)
+        hipLaunchKernelGGL(k4_trace_brick, dim3(blocks), dim3(256), 0, c->stream, k);
+    else
+        hipLaunchKernelGGL(k4_trace, dim3(blocks), dim3(256), 0, c->stream, k);
     return hipGetLastError();
 }
 
