@@ -1,0 +1,105 @@
+"""Multi-rank path on the CPU (gloo, world_size 2 and 3): level-0 grid broadcast
+from rank 0, per-rank interleaved 64x64 screen tiles, all-gather of the
+rank-compact buffers and the un-permute must reproduce the single-rank frame
+bit for bit.  The per-rank trace here is the CPU oracle (test
+infrastructure); on the GPU the same host logic drives vct_trace_device
+(bench.py, vct.multi.FrameTracer)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _setup(n=16, w=150, h=70):
+    from vct import scenes
+    from vct.camera import Camera
+    s = scenes.atrium()
+    g0, E = scenes.grid_for_unit_box(n)
+    cam = Camera()
+    gb = scenes.raycast_numpy(s, cam, w, h)
+    return s, g0, E, cam, gb
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    for p in (REPO, os.path.join(REPO, "voxel-based-global-illumination_amd")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle as O
+    from vct import multi, scenes
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 16
+    s, g0, E, cam, (pos, nrm, alb) = _setup(n)
+    h, w = pos.shape[:2]
+    # K1 + K2 on rank 0 only, then broadcast the level-0 grid
+    r0 = torch.zeros((n, n, n, 4), dtype=torch.float32)
+    if rank == 0:
+        v, i, m, k = s.arrays()
+        st = O.pipeline(n, g0, E, v, i, m, k, scenes.LIGHT_DIR)
+        r0 = torch.from_numpy(st["r0"].copy())
+    dist.broadcast(r0, src=0)
+    pyr = O.build_mips(n, r0.numpy(), True)           # K3 locally on every rank
+    # trace only this rank's tiles
+    fi, _ = multi.compact_index(w, h, rank, world)
+    mine = np.zeros(h * w, bool)
+    mine[fi] = True
+    pos_l = pos.copy()
+    pos_l.reshape(-1, 4)[~mine, 3] = 0
+    res = O.trace(n, g0, E, r0.numpy(), pyr, pos_l, nrm, alb, cam.position, threads=1)
+    packed = torch.from_numpy(np.concatenate([multi.pack(res["diffuse"], rank, world),
+                                              multi.pack(res["spec"], rank, world)], -1))
+    gathered = [torch.empty_like(packed) for _ in range(world)]
+    dist.all_gather(gathered, packed)
+    frame = multi.untile(torch.stack(gathered).numpy(), w, h, world)
+    np.save(os.path.join(out_dir, f"frame{rank}.npy"), frame)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tiled_broadcast_gather_matches_single_rank(oracle_mod, tmp_path, world):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    O = oracle_mod
+    from vct import scenes
+    n = 16
+    s, g0, E, cam, (pos, nrm, alb) = _setup(n)
+    v, i, m, k = s.arrays()
+    st = O.pipeline(n, g0, E, v, i, m, k, scenes.LIGHT_DIR)
+    ref = O.trace(n, g0, E, st["r0"], st["pyr"], pos, nrm, alb, cam.position)
+    full = np.concatenate([ref["diffuse"], ref["spec"]], -1)
+    for r in range(world):
+        got = np.load(tmp_path / f"frame{r}.npy")
+        assert np.array_equal(got, full), f"rank {r}"
+
+
+@pytest.mark.parametrize("w,h,world", [(150, 70, 2), (64, 64, 3), (1920, 1080, 8), (1, 1, 4), (130, 1, 3)])
+def test_tile_partition_is_exact_cover(w, h, world):
+    from vct import multi
+    seen = np.zeros(w * h, np.int64)
+    for r in range(world):
+        fi, ci = multi.compact_index(w, h, r, world)
+        seen[fi] += 1
+        assert ci.max(initial=-1) < multi.tiles_for_rank(w, h, 0, world) * 64 * 64
+        assert len(np.unique(ci)) == len(ci)
+    assert np.all(seen == 1)
+    # rank 0 holds the largest share
+    assert all(multi.tiles_for_rank(w, h, r, world) <= multi.tiles_for_rank(w, h, 0, world) for r in range(world))
+
+
+def test_tiles_for_rank_matches_c_abi():
+    from vct import multi, tiles_for_rank
+    for (w, h, world) in [(1920, 1080, 1), (1920, 1080, 8), (3840, 2160, 3), (65, 65, 2), (10, 10, 7)]:
+        for r in range(world):
+            assert tiles_for_rank(w, h, r, world) == multi.tiles_for_rank(w, h, r, world)
