@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of K4 variants in ONE process (cdna guide rule 24).
+
+    python tools/ab.py --variants 0,3,1 [--rounds 5 --reps 5] [--gbuffer scene|rand]
+
+Prints the median / min kernel ms per variant and checks every variant's
+output is bit-identical to the first one's.
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "voxel-based-global-illumination_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,3,1")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--w", type=int, default=1920)
+    ap.add_argument("--h", type=int, default=1080)
+    ap.add_argument("--gbuffer", default="scene")
+    ap.add_argument("--scene", default="atrium")
+    a = ap.parse_args()
+    import torch
+    from vct import Context, scenes
+    from vct.camera import Camera
+    variants = [int(v, 0) for v in a.variants.split(",")]
+    g0, E = scenes.grid_for_unit_box(a.n)
+    ctx = Context(a.n, g0, E)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+    ctx.voxelize(*scenes.SCENES[a.scene]().arrays())
+    ctx.inject_directional(scenes.LIGHT_DIR)
+    ctx.build_mips()
+    dev = torch.device("cuda")
+    cam = Camera()
+    if a.gbuffer == "scene":
+        gb = [torch.empty((a.h, a.w, 4), device=dev) for _ in range(3)]
+        ctx.gbuffer_raycast_device(cam, a.w, a.h, scenes.ROUGHNESS, *gb)
+    else:
+        ao, nm = ctx.download_voxels()
+        gb = [torch.from_numpy(x).to(dev) for x in scenes.gbuffer_rand(ao, nm, g0, E, a.w, a.h)]
+    outs = {v: (torch.empty((a.h, a.w, 4), device=dev), torch.empty((a.h, a.w, 4), device=dev)) for v in variants}
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    ctx.trace_device(*gb, a.w, a.h, cam.position, *outs[variants[0]], cone_steps=cnt[0:1], variant=variants[0])
+    torch.cuda.synchronize()
+    steps = int(cnt[0])
+    times = {v: [] for v in variants}
+    for v in variants:   # warm-up
+        ctx.trace_device(*gb, a.w, a.h, cam.position, *outs[v], variant=v)
+    for _ in range(a.rounds):
+        for v in variants:
+            for _ in range(a.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                ctx.trace_device(*gb, a.w, a.h, cam.position, *outs[v], variant=v)
+                e1.record(stream)
+                e1.synchronize()
+                times[v].append(e0.elapsed_time(e1))
+    ref = outs[variants[0]]
+    res = {}
+    for v in variants:
+        t = sorted(times[v])
+        same = bool(torch.equal(outs[v][0], ref[0]) and torch.equal(outs[v][1], ref[1]))
+        res[hex(v)] = {"median_ms": round(t[len(t) // 2], 4), "min_ms": round(t[0], 4),
+                       "Gsteps_s": round(steps / (t[len(t) // 2] * 1e-3) / 1e9, 2), "bitexact_vs_first": same}
+    print(json.dumps({"gbuffer": a.gbuffer, "steps": steps, "variants": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

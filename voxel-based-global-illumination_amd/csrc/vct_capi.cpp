@@ -130,8 +130,9 @@ vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
     for (uint32_t l = g.L + 1; l <= (uint32_t)kMaxLevels; ++l) g.lvl_off[l] = off;
     g.pyr_texels = off;
     const size_t nv = (size_t)g.n * g.n * g.n;
-    hipError_t e = hipMalloc(&g.pyr, off * sizeof(float4));
-    if (e == hipSuccess) e = hipMemset(g.pyr, 0, off * sizeof(float4));
+    // +1 texel: a permanent zero texel after the pyramid (zero border of the LDS-DMA staging)
+    hipError_t e = hipMalloc(&g.pyr, (off + 1) * sizeof(float4));
+    if (e == hipSuccess) e = hipMemset(g.pyr, 0, (off + 1) * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&g.albedo_occ, nv * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&g.normal, nv * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&g.occ_bits, (nv / 64) * 8);

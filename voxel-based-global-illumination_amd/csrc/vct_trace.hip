@@ -21,6 +21,20 @@
 //    zeroed weights on clamped addresses (no out-of-bounds access, no branch).
 #include "vct_internal.h"
 
+// Debug-build counters (make dbg -> vct/libvct_hip_dbg.so): per wave-step path
+// statistics of the LDS variants, read with vct_debug_counters().  Compiled out
+// of the product library.
+#ifdef VCT_DEBUG_COUNTERS
+__device__ unsigned long long vct_dbg_ctr[16];
+#define VCT_DBG(i) do { if ((threadIdx.x & 63) == 0) atomicAdd(&vct_dbg_ctr[i], 1ull); } while (0)
+#else
+#define VCT_DBG(i) do { } while (0)
+#endif
+
+extern "C" __device__ int __ockl_wfred_min_i32(int);   // wave-wide reductions over active lanes (ockl)
+extern "C" __device__ float __ockl_wfred_min_f32(float);
+extern "C" __device__ float __ockl_wfred_max_f32(float);
+
 namespace vct {
 namespace {
 
@@ -31,6 +45,7 @@ __constant__ float c_cones16[16][4] = {VCT_CONES16(VCT_CROW)};
 
 struct TraceK {
     const float4* pyr;
+    const float4* zero;      // one zero texel (the zero border for LDS-DMA staging)
     uint64_t lvl_off[kMaxLevels + 1];
     int n, L;
     float g0x, g0y, g0z, inv_h, tmax;
@@ -46,6 +61,7 @@ struct TraceK {
     float ex, ey, ez;
     int tiles_x, rank, world, n_local_tiles, compact;
     int nd, spec_on, aniso;
+    int brick_log2;          // largest staged brick: 2^brick_log2 texels (6..8)
     float tau_d;
 };
 
@@ -292,9 +308,115 @@ __device__ __forceinline__ float4 brick_tri(const float4* __restrict__ b, float 
     return acc;
 }
 
-// D_l for one level; `lds` = this wave's slots for the level (nf x 64 texels).
-// Must be called in wave-uniform control flow (all 64 lanes).
+// Adaptive brick: the wave's footprint at level l is the box spanned by the
+// active lanes' positions (per-axis min / max of q, reduced once per step; the
+// texel map x -> floor(x * 2^-l - 0.5) is monotonic, so reducing q and mapping
+// gives exactly the min / max corner).  The brick is that box rounded up to
+// power-of-two dims (2..16 per axis) and staged when it holds <= 256 texels
+// (4 texels per lane, 4 KiB per face).  Corners are read at
+// base + {0, 1, dx} + {0, dx*dy} (strides are wave-uniform).
+constexpr int kSlotTexels = 256;
+
+__device__ __forceinline__ int log2_dim(int e) {
+    return e <= 2 ? 1 : (e <= 4 ? 2 : (e <= 8 ? 3 : (e <= 16 ? 4 : 16)));   // 16: never fits
+}
+
+__device__ __forceinline__ float4 brick_tri_s(const float4* __restrict__ b, uint32_t sy, uint32_t sz, float fx,
+                                              float fy, float fz) {
+    const float wx[2] = {1.0f - fx, fx}, wy[2] = {1.0f - fy, fy}, wz[2] = {1.0f - fz, fz};
+    float4 v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = b[(c & 1) + sy * ((c >> 1) & 1) + sz * (c >> 2)];
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float w = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
+        acc.x = fmaf(w, v[c].x, acc.x);
+        acc.y = fmaf(w, v[c].y, acc.y);
+        acc.z = fmaf(w, v[c].z, acc.z);
+        acc.w = fmaf(w, v[c].w, acc.w);
+    }
+    return acc;
+}
+
+// D_l for one level.  `mn` / `mx`: wave-uniform min / max of the active lanes'
+// q.  `lds` = this wave's 3 x kSlotTexels slots.  Wave-uniform control flow only.
 __device__ __forceinline__ float4 level_brick(const TraceK& k, int l, float qx, float qy, float qz, bool active,
+                                              const float (&mn)[3], const float (&mx)[3], bool faces_uniform,
+                                              int ufaces, int fx, int fy, int fz, float wdx, float wdy, float wdz,
+                                              float4* __restrict__ lds) {
+    const float scale = __uint_as_float((uint32_t)(127 - l) << 23);
+    const int nl = k.n >> l;
+    const bool iso = (l == 0 || !k.aniso);
+    int o[3], lb[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        o[a] = __builtin_amdgcn_readfirstlane((int)floorf(mn[a] * scale - 0.5f));
+        const int hi = __builtin_amdgcn_readfirstlane((int)floorf(mx[a] * scale - 0.5f));
+        lb[a] = log2_dim(hi - o[a] + 2);
+    }
+    const int lxy = lb[0] + lb[1], ltot = lxy + lb[2];
+    const bool fits = ltot <= k.brick_log2 && (iso || faces_uniform);
+    VCT_DBG(fits ? 2 : 3);
+    if (!fits) VCT_DBG(4 + (l < 10 ? l : 10));
+    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (fits) {
+        const float4* lvl = k.pyr + k.lvl_off[l];
+        const size_t vl = (size_t)nl * nl * nl;
+        const int lane = threadIdx.x & 63;
+        const int total = 1 << ltot, mxd = (1 << lb[0]) - 1, myd = (1 << lb[1]) - 1;
+        const int nf = iso ? 1 : 3;
+        const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll 1
+        for (int f = 0; f < nf; ++f) {
+            // wave-uniform faces: lanes that trace nothing still stage texels
+            const int face = iso ? 0 : (f == 0 ? (ufaces & 7) : (f == 1 ? ((ufaces >> 3) & 7) : (ufaces >> 6)));
+            const float4* vol = lvl + (size_t)face * vl;
+#pragma unroll
+            for (int it = 0; it < kSlotTexels / 64; ++it) {
+                const int j = lane + 64 * it;
+                if (it == 0 || j < total) {
+                    const int sx = o[0] + (j & mxd), sy = o[1] + ((j >> lb[0]) & myd), sz = o[2] + (j >> lxy);
+                    const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl &&
+                                     (unsigned)sz < (unsigned)nl && j < total;
+                    const uint32_t gi = inb ? (uint32_t)sx + (uint32_t)nl * ((uint32_t)sy + (uint32_t)nl * (uint32_t)sz) : 0u;
+                    const float4 v = vol[gi];
+                    if (j < total) lds[f * kSlotTexels + j] = sel4(inb, v, z4);
+                }
+            }
+        }
+        wave_lds_sync();
+        if (active) {
+            const float cx = qx * scale - 0.5f, cy = qy * scale - 0.5f, cz = qz * scale - 0.5f;
+            const float flx = floorf(cx), fly = floorf(cy), flz = floorf(cz);
+            const uint32_t base = (uint32_t)((int)flx - o[0]) + ((uint32_t)((int)fly - o[1]) << lb[0]) +
+                                  ((uint32_t)((int)flz - o[2]) << lxy);
+            const uint32_t sy = 1u << lb[0], sz = 1u << lxy;
+            const float frx = cx - flx, fry = cy - fly, frz = cz - flz;
+            if (iso) {
+                s = brick_tri_s(lds + base, sy, sz, frx, fry, frz);
+            } else {
+#pragma unroll 1
+                for (int f = 0; f < 3; ++f) {
+                    const float w = f == 0 ? wdx : (f == 1 ? wdy : wdz);
+                    const float4 tf = brick_tri_s(lds + f * kSlotTexels + base, sy, sz, frx, fry, frz);
+                    s.x = fmaf(w, tf.x, s.x);
+                    s.y = fmaf(w, tf.y, s.y);
+                    s.z = fmaf(w, tf.z, s.z);
+                    s.w = fmaf(w, tf.w, s.w);
+                }
+            }
+        }
+        wave_lds_sync();
+    } else if (active) {
+        s = sample_level(k, l, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+    }
+    return s;
+}
+
+// Fixed 4^3 brick (variant 3): D_l for one level; `lds` = this wave's slots (nf x 64 texels).
+// Must be called in wave-uniform control flow (all 64 lanes).
+__device__ __forceinline__ float4 level_brick4(const TraceK& k, int l, float qx, float qy, float qz, bool active,
                                               int first, bool faces_uniform, int ufaces, int fx, int fy, int fz,
                                               float wdx, float wdy, float wdz, float4* __restrict__ lds) {
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);
@@ -303,9 +425,11 @@ __device__ __forceinline__ float4 level_brick(const TraceK& k, int l, float qx, 
     const float flx = floorf(cx), fly = floorf(cy), flz = floorf(cz);
     const int ix = (int)flx, iy = (int)fly, iz = (int)flz;
     const bool iso = (l == 0 || !k.aniso);
-    const int ox = __builtin_amdgcn_readlane(ix, first) - 1;
-    const int oy = __builtin_amdgcn_readlane(iy, first) - 1;
-    const int oz = __builtin_amdgcn_readlane(iz, first) - 1;
+    // brick origin = per-axis minimum corner over the active lanes (wave reduction)
+    const int ox = __ockl_wfred_min_i32(active ? ix : INT_MAX);
+    const int oy = __ockl_wfred_min_i32(active ? iy : INT_MAX);
+    const int oz = __ockl_wfred_min_i32(active ? iz : INT_MAX);
+    (void)first;
     const uint32_t lx = (uint32_t)(ix - ox), ly = (uint32_t)(iy - oy), lz = (uint32_t)(iz - oz);
     const bool fits = __all(!active || (lx <= 2u && ly <= 2u && lz <= 2u)) && (iso || faces_uniform);
     float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -355,6 +479,7 @@ __device__ __forceinline__ float4 level_brick(const TraceK& k, int l, float qx, 
 }
 
 // one cone, wave-synchronous (A.6); same arithmetic as march()
+template <bool FIXED>
 __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, float ox, float oy, float oz,
                                                 float dx, float dy, float dz, float tau, float4& res,
                                                 uint32_t& texels, float4* __restrict__ lds) {
@@ -391,12 +516,32 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         const bool lvl_uniform = __all(!active || l0 == l0f);
         const bool two = fr > 0.0f && l0 < k.L;
         float4 s;
-        if (lvl_uniform) {
-            s = level_brick(k, l0f, qx, qy, qz, active, first, faces_uniform, f0, fx, fy, fz, wdx, wdy, wdz, lds);
+        if (FIXED && lvl_uniform) {
+            s = level_brick4(k, l0f, qx, qy, qz, active, first, faces_uniform, f0, fx, fy, fz, wdx, wdy, wdz, lds);
             if (__any(active && two)) {
                 const int l1 = l0f + 1 <= k.L ? l0f + 1 : k.L;
-                float4 s1 = level_brick(k, l1, qx, qy, qz, active && two, first, faces_uniform, f0, fx, fy, fz,
-                                        wdx, wdy, wdz, lds + 3 * 64);
+                float4 s1 = level_brick4(k, l1, qx, qy, qz, active && two, first, faces_uniform, f0, fx, fy, fz,
+                                         wdx, wdy, wdz, lds + 3 * 64);
+                if (active && two) {
+                    const float omf = 1.0f - fr;
+                    s.x = fmaf(fr, s1.x, omf * s.x);
+                    s.y = fmaf(fr, s1.y, omf * s.y);
+                    s.z = fmaf(fr, s1.z, omf * s.z);
+                    s.w = fmaf(fr, s1.w, omf * s.w);
+                }
+            }
+        } else if (lvl_uniform) {
+            // footprint box of the active lanes, shared by both levels of this step
+            const float inf = __builtin_inff();
+            const float mn[3] = {__ockl_wfred_min_f32(active ? qx : inf), __ockl_wfred_min_f32(active ? qy : inf),
+                                 __ockl_wfred_min_f32(active ? qz : inf)};
+            const float mx[3] = {__ockl_wfred_max_f32(active ? qx : -inf), __ockl_wfred_max_f32(active ? qy : -inf),
+                                 __ockl_wfred_max_f32(active ? qz : -inf)};
+            s = level_brick(k, l0f, qx, qy, qz, active, mn, mx, faces_uniform, f0, fx, fy, fz, wdx, wdy, wdz, lds);
+            if (__any(active && two)) {
+                const int l1 = l0f + 1 <= k.L ? l0f + 1 : k.L;
+                float4 s1 = level_brick(k, l1, qx, qy, qz, active && two, mn, mx, faces_uniform, f0, fx, fy, fz,
+                                        wdx, wdy, wdz, lds);
                 if (active && two) {
                     const float omf = 1.0f - fr;
                     s.x = fmaf(fr, s1.x, omf * s.x);
@@ -432,8 +577,232 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     return steps;
 }
 
-__global__ void __launch_bounds__(256) k4_trace_brick(TraceK k) {
-    __shared__ float4 lds_all[4][kBrickSlots * 64];
+// ===========================================================================
+// Variant 2: brick staging with LDS-DMA prefetch of the NEXT step's bricks
+// ===========================================================================
+// Variant 0 pays two dependent memory round trips per step (global load ->
+// ds_write -> ds_read) and the waves sit in s_waitcnt ~45 % of their cycles.
+// Here the bricks of step k+1 are fetched while step k computes: the next t
+// (t + D/2) is known before step k samples, so the first active lane's next
+// position and mip pair give the next brick origins, and the wave issues
+// global_load_lds_dwordx4 (one texel per lane straight into LDS, no VGPRs) into
+// the other half of a double-buffered LDS ring.  A step consumes its buffer
+// behind a counted s_waitcnt vmcnt(n_next) that leaves the prefetch in flight.
+// The DMA is inline asm so the compiler neither waits vmcnt(0) before every
+// ds_read (what it does for the builtin) nor reorders around it ("memory").
+// The plan is speculative: if the active lanes' levels or footprints do not
+// match it, the step falls back to per-lane gathers; results stay bit-exact.
+struct Plan {
+    int lA, lB;              // levels staged in slots 0..2 / 3..5 (lB = -1: none)
+    int ax, ay, az;          // brick origins
+    int bx, by, bz;
+    int n;                   // LDS-DMA instructions issued for this plan
+};
+
+__device__ __forceinline__ void glds16(uint32_t lds_addr, const float4* g) {
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr), "v"(g) : "memory", "m0");
+}
+
+__device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n wave-uniform in 0..6
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    }
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const float4* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float4*)p;
+}
+
+// stage level l's brick (origin = min corner over the `act` lanes' positions q)
+// into `slot0`; returns the number of LDS-DMA instructions issued
+__device__ __forceinline__ int stage_dma(const TraceK& k, int l, float qx, float qy, float qz, bool act,
+                                         int ufaces, const float4* slot0, int& ox, int& oy, int& oz) {
+    const float scale = __uint_as_float((uint32_t)(127 - l) << 23);
+    const int nl = k.n >> l;
+    // origin = per-axis minimum corner over the lanes expected to sample (act)
+    ox = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_i32(act ? (int)floorf(qx * scale - 0.5f) : INT_MAX));
+    oy = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_i32(act ? (int)floorf(qy * scale - 0.5f) : INT_MAX));
+    oz = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_i32(act ? (int)floorf(qz * scale - 0.5f) : INT_MAX));
+    const int lane = threadIdx.x & 63;
+    const int sx = ox + (lane & 3), sy = oy + ((lane >> 2) & 3), sz = oz + (lane >> 4);
+    const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
+    const uint32_t gi = (uint32_t)sx + (uint32_t)nl * ((uint32_t)sy + (uint32_t)nl * (uint32_t)sz);
+    const float4* lvl = k.pyr + k.lvl_off[l];
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_u32(slot0));
+    if (l == 0 || !k.aniso) {
+        glds16(base, inb ? lvl + gi : k.zero);
+        return 1;
+    }
+    const size_t vl = (size_t)nl * nl * nl;
+    const int ux = ufaces & 7, uy = (ufaces >> 3) & 7, uz = ufaces >> 6;
+    glds16(base, inb ? lvl + (size_t)ux * vl + gi : k.zero);
+    glds16(base + 1024, inb ? lvl + (size_t)uy * vl + gi : k.zero);
+    glds16(base + 2048, inb ? lvl + (size_t)uz * vl + gi : k.zero);
+    return 3;
+}
+
+// plan + issue the bricks of a step: lanes `act` at positions q, (uniform) cone size D
+__device__ __forceinline__ Plan plan_issue(const TraceK& k, float qx, float qy, float qz, bool act, float D,
+                                           int ufaces, const float4* buf) {
+    Plan p;
+    float m = spec_log2(D);
+    if (m > (float)k.L) m = (float)k.L;
+    const int l0 = (int)m;
+    const float fr = m - (float)l0;
+    p.lA = __builtin_amdgcn_readfirstlane(l0);
+    const bool two = __builtin_amdgcn_readfirstlane((fr > 0.0f && l0 < k.L) ? 1 : 0) != 0;
+    p.n = stage_dma(k, p.lA, qx, qy, qz, act, ufaces, buf, p.ax, p.ay, p.az);
+    p.lB = -1;
+    p.bx = p.by = p.bz = 0;
+    if (two) {
+        p.lB = p.lA + 1;
+        p.n += stage_dma(k, p.lB, qx, qy, qz, act, ufaces, buf + 3 * 64, p.bx, p.by, p.bz);
+    }
+    return p;
+}
+
+// D_l from a staged brick (origin o*) if every lane in `need` fits; `ok` reports it
+__device__ __forceinline__ float4 level_from_plan(const TraceK& k, int l, float qx, float qy, float qz, bool need,
+                                                  int ox, int oy, int oz, float wdx, float wdy, float wdz,
+                                                  const float4* __restrict__ slot0) {
+    const float scale = __uint_as_float((uint32_t)(127 - l) << 23);
+    const float cx = qx * scale - 0.5f, cy = qy * scale - 0.5f, cz = qz * scale - 0.5f;
+    const float flx = floorf(cx), fly = floorf(cy), flz = floorf(cz);
+    const uint32_t lx = (uint32_t)((int)flx - ox), ly = (uint32_t)((int)fly - oy), lz = (uint32_t)((int)flz - oz);
+    float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (need) {
+        const uint32_t base = lx + 4u * ly + 16u * lz;
+        const float frx = cx - flx, fry = cy - fly, frz = cz - flz;
+        if (l == 0 || !k.aniso) return brick_tri(slot0 + base, frx, fry, frz);
+#pragma unroll 1
+        for (int f = 0; f < 3; ++f) {
+            const float w = f == 0 ? wdx : (f == 1 ? wdy : wdz);
+            const float4 tf = brick_tri(slot0 + 64 * f + base, frx, fry, frz);
+            s.x = fmaf(w, tf.x, s.x);
+            s.y = fmaf(w, tf.y, s.y);
+            s.z = fmaf(w, tf.z, s.z);
+            s.w = fmaf(w, tf.w, s.w);
+        }
+    }
+    return s;
+}
+
+__device__ __forceinline__ bool fits_plan(int l, float qx, float qy, float qz, bool need, int ox, int oy, int oz) {
+    const float scale = __uint_as_float((uint32_t)(127 - l) << 23);
+    const uint32_t lx = (uint32_t)((int)floorf(qx * scale - 0.5f) - ox);
+    const uint32_t ly = (uint32_t)((int)floorf(qy * scale - 0.5f) - oy);
+    const uint32_t lz = (uint32_t)((int)floorf(qz * scale - 0.5f) - oz);
+    return __all(!need || (lx <= 2u && ly <= 2u && lz <= 2u));
+}
+
+__device__ __forceinline__ uint32_t march_pf(const TraceK& k, bool valid, float ox, float oy, float oz, float dx,
+                                             float dy, float dz, float tau, float4& res, uint32_t& texels,
+                                             float4* __restrict__ ring) {
+    const float tau2 = 2.0f * tau;
+    const float nf = (float)k.n, Lf = (float)k.L;
+    const int fx = dx >= 0.0f ? VCT_FACE_PX : VCT_FACE_NX;
+    const int fy = dy >= 0.0f ? VCT_FACE_PY : VCT_FACE_NY;
+    const int fz = dz >= 0.0f ? VCT_FACE_PZ : VCT_FACE_NZ;
+    const float wdx = dx * dx, wdy = dy * dy, wdz = dz * dz;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f, a = 0.0f, t = 1.0f;
+    uint32_t steps = 0;
+    bool active = valid;
+    const unsigned long long vm = __ballot(valid);
+    if (vm == 0ull) { res = make_float4(0.0f, 0.0f, 0.0f, 0.0f); return 0; }
+    const int fcode = fx | (fy << 3) | (fz << 6);
+    const int f0 = __builtin_amdgcn_readlane(fcode, __builtin_ctzll(vm));
+    const bool faces_uniform = __all(!valid || fcode == f0);
+    int buf = 0;
+    Plan cur;
+    {   // plan of step 0 from the first valid lane
+        const int fl = __builtin_ctzll(vm);
+        const float D0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fmaxf(1.0f, tau2 * t)), fl));
+        cur = plan_issue(k, ox + dx * t, oy + dy * t, oz + dz * t, valid, D0, f0, ring);
+    }
+    for (;;) {
+        const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
+        if (active) {
+            if (!(a < VCT_ALPHA_STOP)) active = false;
+            else if (!(t <= k.tmax)) active = false;
+            else if (!(qx >= 0.0f && qx <= nf && qy >= 0.0f && qy <= nf && qz >= 0.0f && qz <= nf)) active = false;
+        }
+        const unsigned long long am = __ballot(active);
+        if (am == 0ull) break;
+        const int first = __builtin_ctzll(am);
+        const float D = fmaxf(1.0f, tau2 * t);
+        float m = spec_log2(D);
+        if (m > Lf) m = Lf;
+        const int l0 = (int)m;
+        const float fr = m - (float)l0;
+        const bool two = fr > 0.0f && l0 < k.L;
+        // does the prefetched plan serve every active lane?
+        bool ok = faces_uniform && __all(!active || l0 == cur.lA) && (cur.lB >= 0 || !__any(active && two));
+        if (ok) ok = fits_plan(cur.lA, qx, qy, qz, active, cur.ax, cur.ay, cur.az);
+        if (ok && cur.lB >= 0) ok = fits_plan(cur.lB, qx, qy, qz, active && two, cur.bx, cur.by, cur.bz);
+        // prefetch the next step's bricks (speculative, first active lane)
+        const float tn = t + VCT_STEP_SCALE * D;
+        const float Dn = fmaxf(1.0f, tau2 * tn);
+        const float nD = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(Dn), first));
+        const float4* cbuf = ring + buf * (kBrickSlots * 64);
+        const Plan nxt = plan_issue(k, ox + dx * tn, oy + dy * tn, oz + dz * tn, active, nD, f0,
+                                    ring + (buf ^ 1) * (kBrickSlots * 64));
+        wait_vm(nxt.n);                 // this step's bricks have landed; the next step's stay in flight
+        float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        VCT_DBG(ok ? 0 : 1);
+        if (ok) {
+            s = level_from_plan(k, cur.lA, qx, qy, qz, active, cur.ax, cur.ay, cur.az, wdx, wdy, wdz, cbuf);
+            if (cur.lB >= 0) {
+                const float4 s1 = level_from_plan(k, cur.lB, qx, qy, qz, active && two, cur.bx, cur.by, cur.bz,
+                                                  wdx, wdy, wdz, cbuf + 3 * 64);
+                if (active && two) {
+                    const float omf = 1.0f - fr;
+                    s.x = fmaf(fr, s1.x, omf * s.x);
+                    s.y = fmaf(fr, s1.y, omf * s.y);
+                    s.z = fmaf(fr, s1.z, omf * s.z);
+                    s.w = fmaf(fr, s1.w, omf * s.w);
+                }
+            }
+        } else if (active) {
+            s = sample_level(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+            if (two) {
+                const float4 s1 = sample_level(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+                const float omf = 1.0f - fr;
+                s.x = fmaf(fr, s1.x, omf * s.x);
+                s.y = fmaf(fr, s1.y, omf * s.y);
+                s.z = fmaf(fr, s1.z, omf * s.z);
+                s.w = fmaf(fr, s1.w, omf * s.w);
+            }
+        }
+        // every lane's reads of this buffer are done before the next iteration
+        // re-targets it (the DMA of step k+2 goes into this buffer)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (active) {
+            texels += (l0 == 0 || !k.aniso) ? 8u : 24u;
+            if (two) texels += k.aniso ? 24u : 8u;
+            const float oma = 1.0f - a;
+            cr = fmaf(oma, s.x, cr);
+            cg = fmaf(oma, s.y, cg);
+            cb = fmaf(oma, s.z, cb);
+            a = fmaf(oma, s.w, a);
+            t = tn;
+            ++steps;
+        }
+        cur = nxt;
+        buf ^= 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the speculative prefetch
+    res = make_float4(cr, cg, cb, a);
+    return steps;
+}
+
+// K4 kernel for the LDS variants: V = 0 brick staging, V = 2 brick staging + DMA prefetch
+template <int V>
+__global__ void __launch_bounds__(256) k4_trace_lds(TraceK k) {
+    __shared__ float4 lds_all[4][V == 2 ? 2 * kBrickSlots * 64 : (V == 3 ? kBrickSlots * 64 : 3 * kSlotTexels)];
     const uint32_t nb = gridDim.x, b = blockIdx.x;
     const uint32_t xcd = b & 7, q = nb >> 3, r = nb & 7;
     const uint32_t rb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
@@ -474,7 +843,8 @@ __global__ void __launch_bounds__(256) k4_trace_brick(TraceK k) {
             const float dy = (cn * ny + ct * Ty) + cb * By;
             const float dz = (cn * nz + ct * Tz) + cb * Bz;
             float4 res;
-            steps += march_brick(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds);
+            if constexpr (V == 2) steps += march_pf(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds);
+            else steps += march_brick<V == 3>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds);
             ir = fmaf(wk, res.x, ir);
             ig = fmaf(wk, res.y, ig);
             ib = fmaf(wk, res.z, ib);
@@ -492,7 +862,8 @@ __global__ void __launch_bounds__(256) k4_trace_brick(TraceK k) {
             const float rough = valid ? k.alb[pix].w : 0.1f;
             const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
             float4 res;
-            steps += march_brick(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds);
+            if constexpr (V == 2) steps += march_pf(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds);
+            else steps += march_brick<V == 3>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds);
             sout = sel4(valid, res, sout);
         }
     }
@@ -509,6 +880,7 @@ __global__ void __launch_bounds__(256) k4_trace_brick(TraceK k) {
         uint32_t wt = wave_sum_u32(texels);
         if (lane == 0 && wt) atomicAdd(k.texels_total, (unsigned long long)wt);
     }
+    if constexpr (V == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // [world][max_tiles][64*64] rank-compact tiles -> [h][w] frame
@@ -609,6 +981,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     const Grid& g = c->grid;
     TraceK k;
     k.pyr = g.pyr;
+    k.zero = g.pyr + g.pyr_texels;
     for (int i = 0; i <= kMaxLevels; ++i) k.lvl_off[i] = g.lvl_off[i];
     k.n = (int)g.n; k.L = (int)g.L;
     k.g0x = g.g0[0]; k.g0y = g.g0[1]; k.g0z = g.g0[2];
@@ -629,13 +1002,21 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.nd = (int)c->cfg.n_diffuse;
     k.spec_on = c->cfg.specular ? 1 : 0;
     k.aniso = g.aniso;
+    // variant bits 8..11: brick size cap (log2 texels); 0 = default
+    const uint32_t cap = (a->variant >> 8) & 0xf;
+    k.brick_log2 = cap ? (int)(cap > 8 ? 8 : cap) : 6;
     k.tau_d = c->cfg.n_diffuse == 16 ? VCT_TAN20 : VCT_TAN30;
     if (nlt == 0) return hipSuccess;
     const uint32_t blocks = nlt * 16;
-    if (a->variant == 0)
-        hipLaunchKernelGGL(k4_trace_brick, dim3(blocks), dim3(256), 0, c->stream, k);
-    else
+    const uint32_t kv = a->variant & 0xff;
+    if (kv == 1)
         hipLaunchKernelGGL(k4_trace, dim3(blocks), dim3(256), 0, c->stream, k);
+    else if (kv == 2)
+        hipLaunchKernelGGL(k4_trace_lds<2>, dim3(blocks), dim3(256), 0, c->stream, k);
+    else if (kv == 3)
+        hipLaunchKernelGGL(k4_trace_lds<3>, dim3(blocks), dim3(256), 0, c->stream, k);
+    else
+        hipLaunchKernelGGL(k4_trace_lds<0>, dim3(blocks), dim3(256), 0, c->stream, k);
     return hipGetLastError();
 }
 
@@ -670,3 +1051,14 @@ hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_
 }
 
 }  // namespace vct
+
+#ifdef VCT_DEBUG_COUNTERS
+extern "C" int vct_debug_counters(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vct_dbg_ctr), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvct_hip.so")
+LIB_PATH = os.environ.get("VCT_LIB") or os.path.join(_HERE, "libvct_hip.so")
 
 # every symbol include/vct.h declares (checked by tests/test_abi.py)
 EXPORTS = (
