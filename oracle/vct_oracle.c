@@ -370,6 +370,38 @@ static void trilinear(const float* vol, uint32_t nl, v3 q, float scale, float ou
             }
 }
 
+/* Directional trilinear sample of an anisotropic level (A.5): the three faces
+ * selected by the signs of d are combined PER CORNER TEXEL,
+ *   v = fmaf(d.z^2, Fz, fmaf(d.y^2, Fy, d.x^2 * Fx)),
+ * and the combined texels are trilinearly filtered like T_l.  (Filtering is
+ * linear, so this equals sum_f w_f T_l(F_f); fixing the order this way lets
+ * a wave whose lanes share one direction combine each texel once.) */
+static void trilinear_dir(const float* lvl, size_t vl, uint32_t nl, v3 q, float scale, const int face[3],
+                          const float wd[3], float out[4]) {
+    float cx = q.x * scale - 0.5f, cy = q.y * scale - 0.5f, cz = q.z * scale - 0.5f;
+    float fx0 = floorf(cx), fy0 = floorf(cy), fz0 = floorf(cz);
+    int ix = (int)fx0, iy = (int)fy0, iz = (int)fz0;
+    float fx = cx - fx0, fy = cy - fy0, fz = cz - fz0;
+    float wx[2] = {1.0f - fx, fx}, wy[2] = {1.0f - fy, fy}, wz[2] = {1.0f - fz, fz};
+    out[0] = out[1] = out[2] = out[3] = 0.0f;
+    for (int dz = 0; dz < 2; ++dz)
+        for (int dy = 0; dy < 2; ++dy)
+            for (int dx = 0; dx < 2; ++dx) {
+                int x = ix + dx, y = iy + dy, z = iz + dz;
+                if (x < 0 || y < 0 || z < 0 || x >= (int)nl || y >= (int)nl || z >= (int)nl) continue;
+                float w = (wx[dx] * wy[dy]) * wz[dz];
+                const float* tX = texel(lvl + (size_t)face[0] * vl, nl, (uint32_t)x, (uint32_t)y, (uint32_t)z);
+                const float* tY = texel(lvl + (size_t)face[1] * vl, nl, (uint32_t)x, (uint32_t)y, (uint32_t)z);
+                const float* tZ = texel(lvl + (size_t)face[2] * vl, nl, (uint32_t)x, (uint32_t)y, (uint32_t)z);
+                for (int c = 0; c < 4; ++c) {
+                    float v = wd[0] * tX[c];
+                    v = fmaf(wd[1], tY[c], v);
+                    v = fmaf(wd[2], tZ[c], v);
+                    out[c] = fmaf(w, v, out[c]);
+                }
+            }
+}
+
 /* D_l(q, d): level 0 isotropic; level >= 1 directional (aniso) or isotropic */
 static void sample_level(const tracer* tr, uint32_t l, v3 q, const int face[3], const float wd[3],
                          float out[4]) {
@@ -378,17 +410,7 @@ static void sample_level(const tracer* tr, uint32_t l, v3 q, const int face[3], 
     const float scale = ldexpf(1.0f, -(int)l);
     const float* lvl = tr->pyr + vo_level_offset(tr->n, tr->aniso, l);
     if (!tr->aniso) { trilinear(lvl, nl, q, scale, out); return; }
-    const size_t vl = (size_t)nl * nl * nl * 4;
-    float tx[4], ty[4], tz[4];
-    trilinear(lvl + (size_t)face[0] * vl, nl, q, scale, tx);
-    trilinear(lvl + (size_t)face[1] * vl, nl, q, scale, ty);
-    trilinear(lvl + (size_t)face[2] * vl, nl, q, scale, tz);
-    for (int c = 0; c < 4; ++c) {
-        float s = wd[0] * tx[c];
-        s = fmaf(wd[1], ty[c], s);
-        s = fmaf(wd[2], tz[c], s);
-        out[c] = s;
-    }
+    trilinear_dir(lvl, (size_t)nl * nl * nl * 4, nl, q, scale, face, wd, out);
 }
 
 /* one cone from o along d with half-angle tangent tau; returns step count */

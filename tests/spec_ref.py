@@ -283,20 +283,37 @@ class Tracer:
                     acc = [fmaf(wc, float(t[k]), acc[k]) for k in range(4)]
         return acc
 
+    def _tri_dir(self, vols, q, scale, wd):
+        """directional sample: faces combined per corner texel, then trilinear"""
+        nl = vols[0].shape[0]
+        c = [f32(f32(q[i] * scale) - 0.5) for i in range(3)]
+        fl = [float(math.floor(v)) for v in c]
+        i0 = [int(v) for v in fl]
+        fr = [f32(c[i] - fl[i]) for i in range(3)]
+        w = [(f32(1.0 - fr[i]), fr[i]) for i in range(3)]
+        acc = [0.0, 0.0, 0.0, 0.0]
+        for dz in range(2):
+            for dy in range(2):
+                for dx in range(2):
+                    x, y, z = i0[0] + dx, i0[1] + dy, i0[2] + dz
+                    if not (0 <= x < nl and 0 <= y < nl and 0 <= z < nl):
+                        continue
+                    wc = f32(f32(w[0][dx] * w[1][dy]) * w[2][dz])
+                    tx, ty, tz = (vols[f][z, y, x] for f in range(3))
+                    for k in range(4):
+                        v = f32(wd[0] * float(tx[k]))
+                        v = fmaf(wd[1], float(ty[k]), v)
+                        v = fmaf(wd[2], float(tz[k]), v)
+                        acc[k] = fmaf(wc, v, acc[k])
+        return acc
+
     def _level(self, l, q, faces, wd):
         scale = 2.0 ** -l
         if l == 0:
             return self._tri(self.r0, q, 1.0)
         if not self.aniso:
             return self._tri(self.mips[l][0], q, scale)
-        ts = [self._tri(self.mips[l][faces[i]], q, scale) for i in range(3)]
-        out = []
-        for k in range(4):
-            s = f32(wd[0] * ts[0][k])
-            s = fmaf(wd[1], ts[1][k], s)
-            s = fmaf(wd[2], ts[2][k], s)
-            out.append(s)
-        return out
+        return self._tri_dir([self.mips[l][faces[i]] for i in range(3)], q, scale, wd)
 
     def march(self, o, d, tau):
         tau2 = f32(2.0 * tau)
