@@ -110,10 +110,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one process per GPU; VCT_DIST_BACKEND=gloo rehearses the N>1 path with
+    # several ranks on one device (RCCL refuses two ranks per GPU)
+    backend = os.environ.get("VCT_DIST_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
+    dev_index = local_rank % ndev if backend != "nccl" else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    local_rank = dev_index
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from vct import Context, scenes
     from vct.camera import Camera
@@ -209,7 +218,7 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("config") == [n, w, h, args.scene, args.gbuffer, args.variant]:
+            if tj.get("config") == [n, w, h, args.scene, args.gbuffer, args.variant, world]:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None

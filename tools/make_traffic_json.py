@@ -23,7 +23,7 @@ def main():
     s = json.loads(subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), d, "k4_trace"],
                                   capture_output=True, text=True, check=True).stdout)
     rec = {
-        "config": [n, w, h, scene, gbuf, variant],
+        "config": [n, w, h, scene, gbuf, variant, 1],
         "source": os.path.relpath(d, REPO),
         "FETCH_SIZE_KiB": s.get("FETCH_SIZE"), "WRITE_SIZE_KiB": s.get("WRITE_SIZE"),
         "hbm_bytes_per_launch": int(2 * s["FETCH_SIZE"] * 1024 + s["WRITE_SIZE"] * 1024),

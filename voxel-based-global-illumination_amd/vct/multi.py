@@ -92,8 +92,12 @@ class FrameTracer:
 
     def gather(self):
         if self.world > 1:
-            self.dist.all_gather_into_tensor(self.diff_g, self.diff_c)
-            self.dist.all_gather_into_tensor(self.spec_g, self.spec_c)
+            if self.dist.get_backend() == "nccl":          # RCCL over xGMI
+                self.dist.all_gather_into_tensor(self.diff_g, self.diff_c)
+                self.dist.all_gather_into_tensor(self.spec_g, self.spec_c)
+            else:                                          # gloo (CPU-side rehearsal of the same path)
+                self.dist.all_gather(list(self.diff_g.chunk(self.world)), self.diff_c)
+                self.dist.all_gather(list(self.spec_g.chunk(self.world)), self.spec_c)
             src_d, src_s = self.diff_g, self.spec_g
         else:
             src_d, src_s = self.diff_c, self.spec_c
