@@ -69,11 +69,28 @@ def test_mips_constant_kat_gpu(gpu_ready):
 
 
 def _gbuf(kind, s, ctx_or_ref, g0, E, w, h):
+    """G-buffers that drive each K4 brick mode: "scene" (flat surfaces: combined
+    faces, brick cache), "rand" (per-lane gathers), "mirror" (lanes with normals
+    +-n_x: equal d^2, different faces), "jitter" (one axis of the normal near
+    zero with random sign: four-face bricks)."""
     from vct import scenes
     from vct.camera import Camera
     cam = Camera()
     if kind == "scene":
         return scenes.raycast_numpy(s, cam, w, h), cam
+    if kind in ("mirror", "jitter"):
+        pos, nrm, alb = scenes.raycast_numpy(s, cam, w, h)
+        yy, xx = np.mgrid[0:h, 0:w]
+        if kind == "mirror":
+            sgn = np.where((xx + yy) % 2 == 0, 1.0, -1.0)
+            nv = np.stack([0.6 * sgn, np.full_like(sgn, 0.8), np.zeros_like(sgn)], -1)
+        else:
+            rng = np.random.default_rng(5)
+            nv = np.stack([rng.uniform(-0.05, 0.05, (h, w)), np.full((h, w), 0.9), np.full((h, w), 0.4)], -1)
+            nv /= np.linalg.norm(nv, axis=-1, keepdims=True)
+        nrm = nrm.copy()
+        nrm[..., :3] = np.where(pos[..., 3:4] != 0, nv, nrm[..., :3]).astype(np.float32)
+        return (pos, nrm, alb), cam
     ao, nm = ctx_or_ref
     return scenes.gbuffer_rand(ao, nm, g0, E, w, h, seed=42), cam
 
@@ -106,9 +123,10 @@ def test_trace_parity(gpu_ready, oracle_mod, name, n, kind, aniso, nd, spec):
     ctx.close()
 
 
-@pytest.mark.parametrize("kind", ["scene", "rand"])
+@pytest.mark.parametrize("kind", ["scene", "rand", "mirror", "jitter"])
 def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
-    """Both K4 variants (0 = LDS-brick default, 1 = per-lane gather) equal the oracle bit for bit."""
+    """The K4 variants (0 = LDS bricks, 1 = per-lane gathers, 2 = bricks without
+    the four-face union) equal the oracle bit for bit."""
     import torch
     O = oracle_mod
     n, w, h = 64, 160, 96

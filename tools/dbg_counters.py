@@ -4,8 +4,8 @@
     make -C voxel-based-global-illumination_amd dbg
     python tools/dbg_counters.py [--gbuffer scene|rand] [--n 256]
 
-Counters (per wave-step): 0/1 = variant 2 plan served / fell back,
-2/3 = variant 0 brick fit / fell back (per level sample).
+Counters: 0/1 = level-A brick / gather per wave-step, 4.. = gathers per level;
+16.. = per-wave phase clocks (s_memtime) of the default variant.
 """
 import argparse
 import ctypes as C
@@ -14,7 +14,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "voxel-based-global-illumination_amd")
-os.environ["VCT_LIB"] = os.path.join(PKG, "vct", "libvct_hip_dbg.so")
+os.environ["VCT_LIB"] = os.path.join(PKG, "vct", "libvct_hip_clk.so" if "--clk" in sys.argv else "libvct_hip_dbg.so")
 sys.path[:0] = [REPO, PKG]
 
 
@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--gbuffer", default="scene")
+    ap.add_argument("--clk", action="store_true", help="phase clocks (make clk) instead of path counters")
+    ap.add_argument("--variants", default="0")
     a = ap.parse_args()
     import torch
     from vct import Context, _lib, scenes
@@ -31,7 +33,7 @@ def main():
     lib = _lib.load()
     lib.vct_debug_counters.restype = C.c_int
     lib.vct_debug_counters.argtypes = [C.c_void_p, C.c_int]
-    ctr = (C.c_ulonglong * 16)()
+    ctr = (C.c_ulonglong * 40)()
     g0, E = scenes.grid_for_unit_box(a.n)
     ctx = Context(a.n, g0, E)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -49,16 +51,21 @@ def main():
         gb = [torch.from_numpy(x).to(dev) for x in scenes.gbuffer_rand(ao, nm, g0, E, a.w, a.h)]
     d = torch.empty((a.h, a.w, 4), device=dev)
     sp = torch.empty((a.h, a.w, 4), device=dev)
-    for v in (0, 2):
+    for v in [int(x, 0) for x in a.variants.split(",")]:
         torch.cuda.synchronize()
         lib.vct_debug_counters(ctr, 1)
         ctx.trace_device(*gb, a.w, a.h, cam.position, d, sp, variant=v)
         torch.cuda.synchronize()
         lib.vct_debug_counters(ctr, 1)
         c = list(ctr)
-        print(f"variant {v}: plan ok {c[0]} fallback {c[1]} | brick fit {c[2]} fallback {c[3]}")
-        if v == 0:
-            print("  fallback per level:", c[4:15], " would fit a 5^3 brick:", c[15])
+        print(f"variant {v}: level-A brick {c[0]} / gather {c[1]} / staged {c[2]} / cache hit {c[3]}; "
+              f"gathers per level: {c[4:15]}")
+        print(f"  gather reasons: faces not uniform {c[16]}; footprint span (level 0) <=3/<=5/<=9/more {c[18:22]}"
+              f"; (level>0) {c[22:26]}")
+        names = ["head", "geometry", "staging", "lds-sample", "fallback", "tail", "kernel"]
+        tot = max(c[32 + 6], 1)
+        print("  phase cycles (sum over waves):",
+              ", ".join(f"{n} {c[32 + i] / 1e9:.3f}G ({100.0 * c[32 + i] / tot:.1f}%)" for i, n in enumerate(names)))
 
 
 if __name__ == "__main__":

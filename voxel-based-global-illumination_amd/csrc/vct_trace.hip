@@ -38,17 +38,46 @@
 
 // Debug-build counters (make dbg -> vct/libvct_hip_dbg.so, tools/dbg_counters.py):
 // per wave and level sample, which path served it.  Compiled out of the product.
+#if defined(VCT_DEBUG_COUNTERS) || defined(VCT_DEBUG_CLOCK)
+__device__ unsigned long long vct_dbg_ctr[32];
+__device__ unsigned long long vct_dbg_time[8];
+#endif
 #ifdef VCT_DEBUG_COUNTERS
-__device__ unsigned long long vct_dbg_ctr[16];
 #define VCT_DBG(i) do { if ((threadIdx.x & 63) == 0) atomicAdd(&vct_dbg_ctr[i], 1ull); } while (0)
 #else
 #define VCT_DBG(i) do { } while (0)
 #endif
 
+// Clock-build (make clk -> vct/libvct_hip_clk.so) per-wave phase clock
+// (s_memtime cycles), summed over waves: 0 step head, 1 brick geometry,
+// 2 staging (loads -> LDS), 3 LDS sampling, 4 per-lane fallback gathers,
+// 5 step tail, 6 kernel total.  Kept apart from the counters, whose global
+// atomics would land in the memory waits being timed.
+struct PhaseClock {
+#ifdef VCT_DEBUG_CLOCK
+    unsigned long long acc[7] = {}, last = 0, first = 0;
+    __device__ void start() { first = last = __builtin_amdgcn_s_memtime(); }
+    __device__ void mark(int i) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        acc[i] += t - last;
+        last = t;
+    }
+    __device__ void flush() {
+        acc[6] = __builtin_amdgcn_s_memtime() - first;
+        if ((threadIdx.x & 63) == 0)
+            for (int i = 0; i < 7; ++i) atomicAdd(&vct_dbg_time[i], acc[i]);
+    }
+#else
+    __device__ void start() {}
+    __device__ void mark(int) {}
+    __device__ void flush() {}
+#endif
+};
+
 extern "C" __device__ int __ockl_wfred_min_i32(int);   // wave-wide min over the active lanes
 
 #ifndef VCT_K4_MIN_WAVES
-#define VCT_K4_MIN_WAVES 1      // __launch_bounds__ minimum waves per SIMD of K4
+#define VCT_K4_MIN_WAVES 4      // __launch_bounds__ minimum waves per SIMD of K4 (128 VGPRs)
 #endif
 
 namespace vct {
@@ -204,9 +233,23 @@ __device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, f
 }
 
 // ===========================================================================
-// wave-cooperative 4^3 LDS bricks (variant 0)
+// wave-cooperative 4^3 LDS bricks with a two-entry brick cache (variant 0)
 // ===========================================================================
-constexpr int kSlots = 6;                      // level A: slots 0..2, level B: slots 3..5
+// A brick is the 4^3 texel block of one level whose origin is the per-axis
+// minimum corner of the active lanes' 2x2x2 footprints.  Lane j stages texel
+// (j & 3, (j >> 2) & 3, j >> 4): one coalesced 16-B load per face.  Modes:
+//   iso   level 0 / isotropic grid: one slot block (64 texels)
+//   comb  anisotropic, the cone direction is the same for every lane: the
+//         staging lanes combine the three faces (the spec combines per corner
+//         texel), one slot block
+//   faces anisotropic otherwise: one slot block per face any lane selects
+//         (3, or 4 when one axis has lanes on both sides)
+// A staged brick stays in LDS for the following steps of the same cone: level
+// l lives in entry l & 1 (a step's two levels never collide), and a step
+// reuses the entry when it holds level l and every active lane's footprint
+// still lies inside it.  Consecutive steps move ~0.25-1 texel, so a brick
+// typically serves two to four steps.
+constexpr int kEntrySlots = 4 * 64;            // float4 per cache entry (up to 4 face blocks)
 
 // One wave's LDS hand-off (writes -> other lanes' reads, and reads -> next
 // writes): the asm "memory" clobber keeps the compiler from moving DS ops
@@ -216,102 +259,252 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// 8 corners of a staged brick at b (x + 4y + 16z)
-__device__ __forceinline__ void brick_corners(const float4* __restrict__ b, float4 (&v)[8]) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) v[c] = b[(c & 1) + 4 * ((c >> 1) & 1) + 16 * (c >> 2)];
-}
-
 struct ConeCtl {                 // wave-uniform facts about one cone
-    int ufaces;                  // face triple of the first valid lane (packed 3 x 3 bits)
-    bool faces_uniform;          // every valid lane selects those faces
-    bool dir_uniform;            // every valid lane has the same wd = d^2 (bitwise)
+    int funion;                  // faces (bit per VCT_FACE_*) any valid lane selects
+    int nfaces;                  // popcount(funion)
+    int f0, f1, f2, f3;          // the faces of funion in increasing order (first nfaces valid)
+    bool dir_uniform;            // every valid lane has the same wd = d^2 (bitwise) and the same faces
     float uwx, uwy, uwz;         // that wd
 };
 
-// D_l for one level (wave-uniform control flow only).  `lds` = 3 slots of 64 texels.
-__device__ __forceinline__ float4 level_brick(const TraceK& k, int l, float qx, float qy, float qz, bool active,
-                                              const ConeCtl& cc, int fx, int fy, int fz, float wdx, float wdy,
-                                              float wdz, float4* __restrict__ lds) {
-    const float scale = __uint_as_float((uint32_t)(127 - l) << 23);
-    const int nl = k.n >> l;
+struct BrickEntry {
+    int lvl;                     // staged level (-1 = empty)
+    int ox, oy, oz;              // its origin
+};
+struct BrickCache {              // wave-uniform; two named entries (a runtime-indexed array would live in scratch)
+    BrickEntry e0, e1;
+    __device__ BrickEntry get(int e) const {
+        BrickEntry b;
+        b.lvl = e ? e1.lvl : e0.lvl;
+        b.ox = e ? e1.ox : e0.ox;
+        b.oy = e ? e1.oy : e0.oy;
+        b.oz = e ? e1.oz : e0.oz;
+        return b;
+    }
+    __device__ void set(int e, const BrickEntry& v) {
+        e0.lvl = e ? e0.lvl : v.lvl; e1.lvl = e ? v.lvl : e1.lvl;
+        e0.ox = e ? e0.ox : v.ox; e1.ox = e ? v.ox : e1.ox;
+        e0.oy = e ? e0.oy : v.oy; e1.oy = e ? v.oy : e1.oy;
+        e0.oz = e ? e0.oz : v.oz; e1.oz = e ? v.oz : e1.oz;
+    }
+};
+
+struct Corner {                  // one lane's trilinear footprint at one level
+    float fx, fy, fz;
+    int ix, iy, iz;
+};
+
+__device__ __forceinline__ Corner level_corner(int l, float qx, float qy, float qz) {
+    const float scale = __uint_as_float((uint32_t)(127 - l) << 23);   // 2^-l, exact
     const float cx = qx * scale - 0.5f, cy = qy * scale - 0.5f, cz = qz * scale - 0.5f;
     const float flx = floorf(cx), fly = floorf(cy), flz = floorf(cz);
-    const int ix = (int)flx, iy = (int)fly, iz = (int)flz;
-    const bool iso = (l == 0 || !k.aniso);
-    // brick origin = per-axis minimum corner over the active lanes
-    const int ox = __ockl_wfred_min_i32(active ? ix : INT_MAX);
-    const int oy = __ockl_wfred_min_i32(active ? iy : INT_MAX);
-    const int oz = __ockl_wfred_min_i32(active ? iz : INT_MAX);
-    const uint32_t lx = (uint32_t)(ix - ox), ly = (uint32_t)(iy - oy), lz = (uint32_t)(iz - oz);
-    const bool fits = __all(!active || (lx <= 2u && ly <= 2u && lz <= 2u)) && (iso || cc.faces_uniform);
-    VCT_DBG(fits ? 0 : 1);
-    if (!fits) {
-        VCT_DBG(4 + (l < 10 ? l : 10));
-        if (active) return sample_level(k, l, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
-        return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
-    const bool comb = !iso && cc.dir_uniform;
-    VCT_DBG(iso ? 2 : (comb ? 3 : 15));
-    // ---- stage: lane j loads texel (j & 3, (j >> 2) & 3, j >> 4) of the brick
+    Corner c;
+    c.fx = cx - flx; c.fy = cy - fly; c.fz = cz - flz;
+    c.ix = (int)flx; c.iy = (int)fly; c.iz = (int)flz;
+    return c;
+}
+
+__device__ __forceinline__ bool in_brick(const Corner& c, const BrickEntry& b) {
+    return (uint32_t)(c.ix - b.ox) <= 2u && (uint32_t)(c.iy - b.oy) <= 2u && (uint32_t)(c.iz - b.oz) <= 2u;
+}
+
+// Brick origin on one axis without a 64-lane reduction: relative to the first
+// active lane's corner b, the wave fits only if every active lane is within
+// [b-2, b+2]; two ballots then give the minimum exactly (-2, -1 or 0).
+__device__ __forceinline__ int wave_origin(int v, bool active, int fl) {
+    const int b = __builtin_amdgcn_readlane(v, fl);
+    const int d = v - b;
+    return b + (__any(active && d < -1) ? -2 : (__any(active && d < 0) ? -1 : 0));
+}
+
+// the per-axis minimum corner over the active lanes, if every footprint fits the brick there
+__device__ __forceinline__ bool brick_origin(const Corner& c, bool active, BrickEntry& b) {
+    const unsigned long long am = __ballot(active);
+    const int fl = am ? __builtin_ctzll(am) : 0;
+    b.ox = wave_origin(c.ix, active, fl);
+    b.oy = wave_origin(c.iy, active, fl);
+    b.oz = wave_origin(c.iz, active, fl);
+    return __all(!active || in_brick(c, b));
+}
+
+enum { kIso = 0, kComb = 1, kFaces = 2 };
+
+struct Tex4 { float4 a, b, c, d; };
+
+// this lane's staging texel: iso -> a; comb / faces -> faces f0..f3 of the union in a..d
+__device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEntry& be, int mode,
+                                           const ConeCtl& cc) {
+    const int nl = k.n >> l;
     const int lane = threadIdx.x & 63;
-    const int sx = ox + (lane & 3), sy = oy + ((lane >> 2) & 3), sz = oz + (lane >> 4);
+    const int sx = be.ox + (lane & 3), sy = be.oy + ((lane >> 2) & 3), sz = be.oz + (lane >> 4);
     const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
     const uint32_t gi = inb ? (uint32_t)sx + (uint32_t)nl * ((uint32_t)sy + (uint32_t)nl * (uint32_t)sz) : 0u;
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const float4* lvl = k.pyr + k.lvl_off[l];
-    if (iso) {
-        lds[lane] = sel4(inb, lvl[gi], z4);
+    Tex4 t;
+    t.b = t.c = t.d = z4;
+    if (mode == kIso) {
+        t.a = sel4(inb, lvl[gi], z4);
     } else {
-        // the wave-uniform face triple: background lanes stage texels too, so the
-        // faces must not come from the lane's own direction
-        const size_t vl = (size_t)nl * nl * nl;
-        const int ux = cc.ufaces & 7, uy = (cc.ufaces >> 3) & 7, uz = cc.ufaces >> 6;
-        const float4 X = sel4(inb, lvl[(size_t)ux * vl + gi], z4);
-        const float4 Y = sel4(inb, lvl[(size_t)uy * vl + gi], z4);
-        const float4 Z = sel4(inb, lvl[(size_t)uz * vl + gi], z4);
-        if (comb) {
-            lds[lane] = combine3(cc.uwx, cc.uwy, cc.uwz, X, Y, Z);
-        } else {
-            lds[lane] = X;
-            lds[64 + lane] = Y;
-            lds[128 + lane] = Z;
-        }
+        const uint32_t vl = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
+        t.a = sel4(inb, lvl[(uint32_t)cc.f0 * vl + gi], z4);
+        t.b = sel4(inb, lvl[(uint32_t)cc.f1 * vl + gi], z4);
+        t.c = sel4(inb, lvl[(uint32_t)cc.f2 * vl + gi], z4);
+        if (cc.nfaces > 3) t.d = sel4(inb, lvl[(uint32_t)cc.f3 * vl + gi], z4);
     }
-    wave_lds_sync();
-    float4 acc = z4;
-    if (active) {
-        float wc[8];
-        corner_weights(cx - flx, cy - fly, cz - flz, wc);
-        const float4* b = lds + (lx + 4u * ly + 16u * lz);
-        if (iso || comb) {
-            float4 v[8];
-            brick_corners(b, v);
+    return t;
+}
+
+__device__ __forceinline__ void stage_store(int mode, const ConeCtl& cc, const Tex4& t, float4* __restrict__ lds) {
+    const int lane = threadIdx.x & 63;
+    if (mode == kIso) {
+        lds[lane] = t.a;
+    } else if (mode == kComb) {     // f0, f1, f2 = the x, y, z faces
+        lds[lane] = combine3(cc.uwx, cc.uwy, cc.uwz, t.a, t.b, t.c);
+    } else {
+        lds[lane] = t.a;
+        lds[64 + lane] = t.b;
+        lds[128 + lane] = t.c;
+        if (cc.nfaces > 3) lds[192 + lane] = t.d;
+    }
+}
+
+// D_l from a staged brick: corner 0 at `b`; faces mode reads the lane's own
+// face blocks at float4 offsets bx, by, bz
+__device__ __forceinline__ float4 brick_sample(const Corner& c, const BrickEntry& be, bool one_slot, int bx,
+                                               int by, int bz, float wdx, float wdy, float wdz,
+                                               const float4* __restrict__ lds) {
+    float wc[8];
+    corner_weights(c.fx, c.fy, c.fz, wc);
+    const float4* b = lds + ((c.ix - be.ox) + 4 * (c.iy - be.oy) + 16 * (c.iz - be.oz));
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (one_slot) {
+        float4 v[8];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) acc_fma(acc, wc[c], v[c]);
-        } else {
+        for (int i = 0; i < 8; ++i) v[i] = b[(i & 1) + 4 * ((i >> 1) & 1) + 16 * (i >> 2)];
 #pragma unroll
-            for (int h = 0; h < 8; h += kCh) {
-                float4 vx[kCh], vy[kCh], vz[kCh];
+        for (int i = 0; i < 8; ++i) acc_fma(acc, wc[i], v[i]);
+    } else {
+        const float4 *X = b + bx, *Y = b + by, *Z = b + bz;
 #pragma unroll
-                for (int c = 0; c < kCh; ++c) {
-                    const int o = ((h + c) & 1) + 4 * (((h + c) >> 1) & 1) + 16 * ((h + c) >> 2);
-                    vx[c] = b[o]; vy[c] = b[64 + o]; vz[c] = b[128 + o];
-                }
+        for (int h = 0; h < 8; h += kCh) {
+            float4 vx[kCh], vy[kCh], vz[kCh];
 #pragma unroll
-                for (int c = 0; c < kCh; ++c) acc_fma(acc, wc[h + c], combine3(wdx, wdy, wdz, vx[c], vy[c], vz[c]));
-                __builtin_amdgcn_sched_barrier(0);
+            for (int i = 0; i < kCh; ++i) {
+                const int o = ((h + i) & 1) + 4 * (((h + i) >> 1) & 1) + 16 * ((h + i) >> 2);
+                vx[i] = X[o]; vy[i] = Y[o]; vz[i] = Z[o];
             }
+#pragma unroll
+            for (int i = 0; i < kCh; ++i) acc_fma(acc, wc[h + i], combine3(wdx, wdy, wdz, vx[i], vy[i], vz[i]));
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
-    wave_lds_sync();
     return acc;
 }
 
+// debug counters 16..: why a level sample fell back to gathers (too many
+// faces; else the footprint span max-min over the active lanes)
+__device__ __forceinline__ void dbg_fallback_reason(const Corner& c, bool active, bool faces_ok, int l) {
+#ifdef VCT_DEBUG_COUNTERS
+    if (!faces_ok) { VCT_DBG(16); return; }
+    const int sx = -__ockl_wfred_min_i32(active ? -c.ix : INT_MIN + 1) - __ockl_wfred_min_i32(active ? c.ix : INT_MAX);
+    const int sy = -__ockl_wfred_min_i32(active ? -c.iy : INT_MIN + 1) - __ockl_wfred_min_i32(active ? c.iy : INT_MAX);
+    const int sz = -__ockl_wfred_min_i32(active ? -c.iz : INT_MIN + 1) - __ockl_wfred_min_i32(active ? c.iz : INT_MAX);
+    const int sp = max(sx, max(sy, sz));
+    const int bin = sp <= 3 ? 0 : (sp <= 5 ? 1 : (sp <= 9 ? 2 : 3));
+    VCT_DBG((l == 0 ? 18 : 22) + bin);
+#endif
+}
+
+// One step's blended sample (1 - fr) D_{l0} + fr D_{l0+1} for a wave-uniform l0.
+// Each level is served from the cache, restaged (both levels' loads in one
+// batch) or, when the wave's footprint does not fit, gathered per lane.
+template <bool UNION>
+__device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx, float qy, float qz, bool active,
+                                              bool two, float fr, const ConeCtl& cc, int fx, int fy, int fz, int bx,
+                                              int by, int bz, float wdx, float wdy, float wdz,
+                                              float4* __restrict__ lds, BrickCache& bc, PhaseClock& pc) {
+    const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const bool activeB = active && two;
+    const bool needB = __any(activeB);
+    const int l1 = l0 + 1;                     // needB implies l0 < L
+    const int aniso_mode = cc.dir_uniform ? kComb : kFaces;
+    const int modeA = (l0 == 0 || !k.aniso) ? kIso : aniso_mode;
+    const int modeB = k.aniso ? aniso_mode : kIso;
+    const bool faces_ok = UNION ? cc.nfaces <= 4 : cc.nfaces == 3;
+    const int eA = l0 & 1, eB = eA ^ 1;
+    float4* ldsA = lds + eA * kEntrySlots;
+    float4* ldsB = lds + eB * kEntrySlots;
+    // level A: cached, restaged, or gathered
+    const Corner cA = level_corner(l0, qx, qy, qz);
+    BrickEntry bA = bc.get(eA);
+    bool useA = bA.lvl == l0 && __all(!active || in_brick(cA, bA));
+    bool stA = false;
+    if (!useA && (modeA != kFaces || faces_ok)) {
+        BrickEntry nb;
+        nb.lvl = l0;
+        if (brick_origin(cA, active, nb)) {
+            bA = nb;
+            bc.set(eA, nb);
+            useA = stA = true;
+        }
+    }
+    Corner cB = cA;
+    BrickEntry bB = bc.get(eB);
+    bool useB = false, stB = false;
+    if (needB) {
+        cB = level_corner(l1, qx, qy, qz);
+        useB = bB.lvl == l1 && __all(!activeB || in_brick(cB, bB));
+        if (!useB && (modeB != kFaces || faces_ok)) {
+            BrickEntry nb;
+            nb.lvl = l1;
+            if (brick_origin(cB, activeB, nb)) {
+                bB = nb;
+                bc.set(eB, nb);
+                useB = stB = true;
+            }
+        }
+    }
+    VCT_DBG(useA ? (stA ? 2 : 3) : 1);
+    pc.mark(1);
+    if (stA && stB) {
+        const Tex4 tA = stage_load(k, l0, bA, modeA, cc);
+        const Tex4 tB = stage_load(k, l1, bB, modeB, cc);
+        stage_store(modeA, cc, tA, ldsA);
+        stage_store(modeB, cc, tB, ldsB);
+        wave_lds_sync();
+    } else if (stA || stB) {
+        const int mode = stA ? modeA : modeB;
+        stage_store(mode, cc, stage_load(k, stA ? l0 : l1, stA ? bA : bB, mode, cc), stA ? ldsA : ldsB);
+        wave_lds_sync();
+    }
+    pc.mark(2);
+    float4 sA = z4, sB = z4;
+    if (useA || useB) {
+        if (useA && active) sA = brick_sample(cA, bA, modeA != kFaces, bx, by, bz, wdx, wdy, wdz, ldsA);
+        if (useB && activeB) sB = brick_sample(cB, bB, modeB != kFaces, bx, by, bz, wdx, wdy, wdz, ldsB);
+        wave_lds_sync();
+    }
+    pc.mark(3);
+    if (!useA) {
+        VCT_DBG(4 + (l0 < 10 ? l0 : 10));
+        dbg_fallback_reason(cA, active, modeA != kFaces || faces_ok, l0);
+        if (active) sA = sample_level(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+    }
+    if (needB && !useB) {
+        VCT_DBG(4 + (l1 < 10 ? l1 : 10));
+        dbg_fallback_reason(cB, activeB, modeB != kFaces || faces_ok, l1);
+        if (activeB) sB = sample_level(k, l1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+    }
+    pc.mark(4);
+    return activeB ? blend(sA, sB, fr) : sA;
+}
+
 // one cone, wave-synchronous (A.6); same arithmetic as march()
+template <bool UNION>
 __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, float ox, float oy, float oz,
                                                 float dx, float dy, float dz, float tau, float4& res,
-                                                uint32_t& texels, float4* __restrict__ lds) {
+                                                uint32_t& texels, float4* __restrict__ lds, PhaseClock& pc) {
     const float tau2 = 2.0f * tau;
     const float nf = (float)k.n, Lf = (float)k.L;
     const int fx = dx >= 0.0f ? VCT_FACE_PX : VCT_FACE_NX;
@@ -321,18 +514,34 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     float cr = 0.0f, cg = 0.0f, cb = 0.0f, a = 0.0f, t = 1.0f;
     uint32_t steps = 0;
     bool active = valid;
-    const unsigned long long vm = __ballot(valid);
     ConeCtl cc;
+    int bx, by, bz;              // this lane's face blocks in a faces-mode brick (float4 offsets)
     {
-        const int fcode = fx | (fy << 3) | (fz << 6);
+        const unsigned long long vm = __ballot(valid);
         const int fl = vm ? __builtin_ctzll(vm) : 0;
-        cc.ufaces = __builtin_amdgcn_readlane(fcode, fl);
+        int u = 0;
+#pragma unroll
+        for (int f = 0; f < 6; ++f) u |= __any(valid && (fx == f || fy == f || fz == f)) ? 1 << f : 0;
+        cc.funion = u;
+        cc.nfaces = __builtin_popcount(u);
+        cc.f0 = __builtin_ctz(u | 64);
+        u &= u - 1;
+        cc.f1 = __builtin_ctz(u | 64);
+        u &= u - 1;
+        cc.f2 = __builtin_ctz(u | 64);
+        u &= u - 1;
+        cc.f3 = __builtin_ctz(u | 64);
+        bx = 64 * __builtin_popcount(cc.funion & ((1 << fx) - 1));
+        by = 64 * __builtin_popcount(cc.funion & ((1 << fy) - 1));
+        bz = 64 * __builtin_popcount(cc.funion & ((1 << fz) - 1));
         cc.uwx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdx), fl));
         cc.uwy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdy), fl));
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
-        cc.faces_uniform = __all(!valid || fcode == cc.ufaces);
-        cc.dir_uniform = __all(!valid || (wdx == cc.uwx && wdy == cc.uwy && wdz == cc.uwz));
+        // same d^2 everywhere AND one face per axis (d and -d share d^2)
+        cc.dir_uniform = __all(!valid || (wdx == cc.uwx && wdy == cc.uwy && wdz == cc.uwz)) && cc.nfaces == 3;
     }
+    BrickCache bc;
+    bc.e0 = bc.e1 = BrickEntry{-1, 0, 0, 0};
     for (;;) {
         const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
         if (active) {
@@ -351,13 +560,9 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         const int l0f = __builtin_amdgcn_readlane(l0, __builtin_ctzll(am));
         float4 s;
         if (__all(!active || l0 == l0f)) {     // wave-uniform mip pair: brick path
-            s = level_brick(k, l0f, qx, qy, qz, active, cc, fx, fy, fz, wdx, wdy, wdz, lds);
-            if (__any(active && two)) {
-                const int l1 = l0f + 1 <= k.L ? l0f + 1 : k.L;
-                const float4 s1 = level_brick(k, l1, qx, qy, qz, active && two, cc, fx, fy, fz, wdx, wdy, wdz,
-                                              lds + 3 * 64);
-                if (active && two) s = blend(s, s1, fr);
-            }
+            pc.mark(0);
+            s = step_bricks<UNION>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy, wdz,
+                                   lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
             s = sample_level(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
             if (two) s = blend(s, sample_level(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz), fr);
@@ -373,6 +578,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
             t = t + VCT_STEP_SCALE * D;
             ++steps;
         }
+        pc.mark(5);
     }
     res = make_float4(cr, cg, cb, a);
     return steps;
@@ -381,9 +587,9 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
 // ===========================================================================
 // the kernel: pixel setup, cone loop, outputs (BRICK = variant 0, else 1)
 // ===========================================================================
-template <bool BRICK, int MINW>
+template <bool BRICK, int MINW, bool UNION = true>
 __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
-    __shared__ float4 lds_all[BRICK ? 4 : 1][BRICK ? kSlots * 64 : 1];
+    __shared__ float4 lds_all[BRICK ? 4 : 1][BRICK ? 2 * kEntrySlots : 1];
     // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid
     const uint32_t nb = gridDim.x, b = blockIdx.x;
     const uint32_t xcd = b & 7, q = nb >> 3, r = nb & 7;
@@ -391,6 +597,8 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
     const uint32_t lt = rb >> 4, sub = rb & 15;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4* lds = lds_all[BRICK ? wave : 0];
+    PhaseClock pc;
+    pc.start();
     const uint32_t px = (sub & 3) * 16 + (wave & 1) * 8 + (lane & 7);
     const uint32_t py = (sub >> 2) * 16 + (wave >> 1) * 8 + (lane >> 3);
     const uint32_t tile = lt * (uint32_t)k.world + (uint32_t)k.rank;
@@ -429,7 +637,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             const float dy = (cn * ny + ct * Ty) + cb * By;
             const float dz = (cn * nz + ct * Tz) + cb * Bz;
             float4 res;
-            if constexpr (BRICK) steps += march_brick(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds);
+            if constexpr (BRICK) steps += march_brick<UNION>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, pc);
             else steps += march(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
             ir = fmaf(wk, res.x, ir);
             ig = fmaf(wk, res.y, ig);
@@ -449,7 +657,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             if (valid) rough = k.alb[pix].w;
             const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
             float4 res;
-            if constexpr (BRICK) steps += march_brick(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds);
+            if constexpr (BRICK) steps += march_brick<UNION>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, pc);
             else steps += march(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
             sout = sel4(valid, res, sout);
         }
@@ -467,6 +675,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
         const uint32_t wt = wave_sum_u32(texels);
         if (lane == 0 && wt) atomicAdd(k.texels_total, (unsigned long long)wt);
     }
+    pc.flush();
 }
 
 }  // namespace
@@ -497,13 +706,9 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
     const uint32_t blocks = nlt * 16;
-    switch (a->variant & 0xff) {   // 0 default; 1 gathers; 2/3 = 0/1 with a 3-waves/SIMD register cap
+    switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers; 2: bricks without the faces union
         case 1: hipLaunchKernelGGL((k4_trace<false, 1>), dim3(blocks), dim3(256), 0, c->stream, k); break;
-        case 2: hipLaunchKernelGGL((k4_trace<true, 3>), dim3(blocks), dim3(256), 0, c->stream, k); break;
-        case 3: hipLaunchKernelGGL((k4_trace<false, 3>), dim3(blocks), dim3(256), 0, c->stream, k); break;
-        case 4: hipLaunchKernelGGL((k4_trace<true, 4>), dim3(blocks), dim3(256), 0, c->stream, k); break;
-        case 5: hipLaunchKernelGGL((k4_trace<true, 5>), dim3(blocks), dim3(256), 0, c->stream, k); break;
-        case 6: hipLaunchKernelGGL((k4_trace<false, 4>), dim3(blocks), dim3(256), 0, c->stream, k); break;
+        case 2: hipLaunchKernelGGL((k4_trace<true, 4, false>), dim3(blocks), dim3(256), 0, c->stream, k); break;
         default: hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES>), dim3(blocks), dim3(256), 0, c->stream, k);
     }
     return hipGetLastError();
@@ -511,12 +716,15 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
 
 }  // namespace vct
 
-#ifdef VCT_DEBUG_COUNTERS
-extern "C" int vct_debug_counters(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+#if defined(VCT_DEBUG_COUNTERS) || defined(VCT_DEBUG_CLOCK)
+extern "C" int vct_debug_counters(unsigned long long* out, int reset) {   // out[40]: 32 counters, 8 clocks
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(vct_dbg_time), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
     if (reset) {
-        unsigned long long z[16] = {};
+        unsigned long long z[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(vct_dbg_ctr), z, sizeof z) != hipSuccess) return -1;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vct_dbg_time), z, sizeof(unsigned long long) * 8) != hipSuccess) return -1;
     }
     return 0;
 }
