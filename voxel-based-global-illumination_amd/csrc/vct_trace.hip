@@ -139,12 +139,22 @@ __device__ __forceinline__ void corner_weights(float fx, float fy, float fz, flo
     for (int c = 0; c < 8; ++c) wc[c] = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
 }
 
+// A texel by index within a level.  O32 (every level < 4 GiB, n <= 512): a
+// 32-bit byte offset from the wave-uniform level base, so the load is
+// global_load with an SGPR base and ONE offset VGPR; else 64-bit addresses.
+template <bool O32>
+__device__ __forceinline__ float4 texel(const float4* __restrict__ lvl, uint32_t i) {
+    if constexpr (O32) return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(lvl) + (i << 4));
+    else return lvl[i];
+}
+
 // ===========================================================================
 // per-lane gathers (variant 1, and the fallback of variant 0)
 // ===========================================================================
 // D_l(q, d) (A.5): level 0 / isotropic = T_l; anisotropic = faces combined per
 // corner texel, then trilinear.  Zero border: out-of-range corners get weight 0
 // on a clamped (valid) address; fmaf(0, v, acc) == acc for the finite texels.
+template <bool O32>
 __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx, float qy, float qz,
                                                int fx, int fy, int fz, float wdx, float wdy, float wdz) {
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
@@ -168,18 +178,22 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
     if (l == 0 || !k.aniso) {
         float4 v[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = lvl[idx[c]];
+        for (int c = 0; c < 8; ++c) v[c] = texel<O32>(lvl, idx[c]);
 #pragma unroll
         for (int c = 0; c < 8; ++c) acc_fma(acc, wc[c], v[c]);
         return acc;
     }
-    const size_t vl = (size_t)nl * nl * nl;
-    const float4 *X = lvl + (size_t)fx * vl, *Y = lvl + (size_t)fy * vl, *Z = lvl + (size_t)fz * vl;
+    const uint32_t vl = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
+    const uint32_t X = (uint32_t)fx * vl, Y = (uint32_t)fy * vl, Z = (uint32_t)fz * vl;
 #pragma unroll
     for (int h = 0; h < 8; h += kCh) {         // kCh corners x 3 faces in flight
         float4 vx[kCh], vy[kCh], vz[kCh];
 #pragma unroll
-        for (int c = 0; c < kCh; ++c) { vx[c] = X[idx[h + c]]; vy[c] = Y[idx[h + c]]; vz[c] = Z[idx[h + c]]; }
+        for (int c = 0; c < kCh; ++c) {
+            vx[c] = texel<O32>(lvl, X + idx[h + c]);
+            vy[c] = texel<O32>(lvl, Y + idx[h + c]);
+            vz[c] = texel<O32>(lvl, Z + idx[h + c]);
+        }
 #pragma unroll
         for (int c = 0; c < kCh; ++c) acc_fma(acc, wc[h + c], combine3(wdx, wdy, wdz, vx[c], vy[c], vz[c]));
         __builtin_amdgcn_sched_barrier(0);     // keep the next chunk's loads below (VGPR budget)
@@ -194,6 +208,7 @@ __device__ __forceinline__ float4 blend(float4 s, float4 s1, float fr) {   // (1
 }
 
 // one cone (A.6), per lane; returns steps, (c, a) in res
+template <bool O32>
 __device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, float oz, float dx, float dy,
                                           float dz, float tau, float4& res, uint32_t& texels) {
     const float tau2 = 2.0f * tau;
@@ -214,11 +229,11 @@ __device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, f
         if (m > Lf) m = Lf;
         const int l0 = (int)m;
         const float fr = m - (float)l0;
-        float4 s = sample_level(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+        float4 s = sample_level<O32>(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
         texels += (l0 == 0 || !k.aniso) ? 8u : 24u;
         if (fr > 0.0f && l0 < k.L) {
             texels += k.aniso ? 24u : 8u;
-            s = blend(s, sample_level(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz), fr);
+            s = blend(s, sample_level<O32>(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz), fr);
         }
         const float oma = 1.0f - a;
         cr = fmaf(oma, s.x, cr);
@@ -332,6 +347,7 @@ enum { kIso = 0, kComb = 1, kFaces = 2 };
 struct Tex4 { float4 a, b, c, d; };
 
 // this lane's staging texel: iso -> a; comb / faces -> faces f0..f3 of the union in a..d
+template <bool O32>
 __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEntry& be, int mode,
                                            const ConeCtl& cc) {
     const int nl = k.n >> l;
@@ -344,13 +360,13 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
     Tex4 t;
     t.b = t.c = t.d = z4;
     if (mode == kIso) {
-        t.a = sel4(inb, lvl[gi], z4);
+        t.a = sel4(inb, texel<O32>(lvl, gi), z4);
     } else {
         const uint32_t vl = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
-        t.a = sel4(inb, lvl[(uint32_t)cc.f0 * vl + gi], z4);
-        t.b = sel4(inb, lvl[(uint32_t)cc.f1 * vl + gi], z4);
-        t.c = sel4(inb, lvl[(uint32_t)cc.f2 * vl + gi], z4);
-        if (cc.nfaces > 3) t.d = sel4(inb, lvl[(uint32_t)cc.f3 * vl + gi], z4);
+        t.a = sel4(inb, texel<O32>(lvl, (uint32_t)cc.f0 * vl + gi), z4);
+        t.b = sel4(inb, texel<O32>(lvl, (uint32_t)cc.f1 * vl + gi), z4);
+        t.c = sel4(inb, texel<O32>(lvl, (uint32_t)cc.f2 * vl + gi), z4);
+        if (cc.nfaces > 3) t.d = sel4(inb, texel<O32>(lvl, (uint32_t)cc.f3 * vl + gi), z4);
     }
     return t;
 }
@@ -419,7 +435,7 @@ __device__ __forceinline__ void dbg_fallback_reason(const Corner& c, bool active
 // One step's blended sample (1 - fr) D_{l0} + fr D_{l0+1} for a wave-uniform l0.
 // Each level is served from the cache, restaged (both levels' loads in one
 // batch) or, when the wave's footprint does not fit, gathered per lane.
-template <bool UNION>
+template <bool O32, bool UNION>
 __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx, float qy, float qz, bool active,
                                               bool two, float fr, const ConeCtl& cc, int fx, int fy, int fz, int bx,
                                               int by, int bz, float wdx, float wdy, float wdz,
@@ -468,14 +484,14 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     VCT_DBG(useA ? (stA ? 2 : 3) : 1);
     pc.mark(1);
     if (stA && stB) {
-        const Tex4 tA = stage_load(k, l0, bA, modeA, cc);
-        const Tex4 tB = stage_load(k, l1, bB, modeB, cc);
+        const Tex4 tA = stage_load<O32>(k, l0, bA, modeA, cc);
+        const Tex4 tB = stage_load<O32>(k, l1, bB, modeB, cc);
         stage_store(modeA, cc, tA, ldsA);
         stage_store(modeB, cc, tB, ldsB);
         wave_lds_sync();
     } else if (stA || stB) {
         const int mode = stA ? modeA : modeB;
-        stage_store(mode, cc, stage_load(k, stA ? l0 : l1, stA ? bA : bB, mode, cc), stA ? ldsA : ldsB);
+        stage_store(mode, cc, stage_load<O32>(k, stA ? l0 : l1, stA ? bA : bB, mode, cc), stA ? ldsA : ldsB);
         wave_lds_sync();
     }
     pc.mark(2);
@@ -489,19 +505,19 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     if (!useA) {
         VCT_DBG(4 + (l0 < 10 ? l0 : 10));
         dbg_fallback_reason(cA, active, modeA != kFaces || faces_ok, l0);
-        if (active) sA = sample_level(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+        if (active) sA = sample_level<O32>(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
     }
     if (needB && !useB) {
         VCT_DBG(4 + (l1 < 10 ? l1 : 10));
         dbg_fallback_reason(cB, activeB, modeB != kFaces || faces_ok, l1);
-        if (activeB) sB = sample_level(k, l1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+        if (activeB) sB = sample_level<O32>(k, l1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
     }
     pc.mark(4);
     return activeB ? blend(sA, sB, fr) : sA;
 }
 
 // one cone, wave-synchronous (A.6); same arithmetic as march()
-template <bool UNION>
+template <bool O32, bool UNION>
 __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, float ox, float oy, float oz,
                                                 float dx, float dy, float dz, float tau, float4& res,
                                                 uint32_t& texels, float4* __restrict__ lds, PhaseClock& pc) {
@@ -561,11 +577,11 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         float4 s;
         if (__all(!active || l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
-            s = step_bricks<UNION>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy, wdz,
+            s = step_bricks<O32, UNION>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy, wdz,
                                    lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
-            s = sample_level(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
-            if (two) s = blend(s, sample_level(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz), fr);
+            s = sample_level<O32>(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+            if (two) s = blend(s, sample_level<O32>(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz), fr);
         }
         if (active) {
             texels += (l0 == 0 || !k.aniso) ? 8u : 24u;
@@ -587,7 +603,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
 // ===========================================================================
 // the kernel: pixel setup, cone loop, outputs (BRICK = variant 0, else 1)
 // ===========================================================================
-template <bool BRICK, int MINW, bool UNION = true>
+template <bool BRICK, int MINW, bool UNION, bool O32>
 __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
     __shared__ float4 lds_all[BRICK ? 4 : 1][BRICK ? 2 * kEntrySlots : 1];
     // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid
@@ -637,8 +653,8 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             const float dy = (cn * ny + ct * Ty) + cb * By;
             const float dz = (cn * nz + ct * Tz) + cb * Bz;
             float4 res;
-            if constexpr (BRICK) steps += march_brick<UNION>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, pc);
-            else steps += march(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
+            if constexpr (BRICK) steps += march_brick<O32, UNION>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, pc);
+            else steps += march<O32>(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
             ir = fmaf(wk, res.x, ir);
             ig = fmaf(wk, res.y, ig);
             ib = fmaf(wk, res.z, ib);
@@ -657,8 +673,8 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             if (valid) rough = k.alb[pix].w;
             const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
             float4 res;
-            if constexpr (BRICK) steps += march_brick<UNION>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, pc);
-            else steps += march(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
+            if constexpr (BRICK) steps += march_brick<O32, UNION>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, pc);
+            else steps += march<O32>(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
             sout = sel4(valid, res, sout);
         }
     }
@@ -706,11 +722,22 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
     const uint32_t blocks = nlt * 16;
-    switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers; 2: bricks without the faces union
-        case 1: hipLaunchKernelGGL((k4_trace<false, 1>), dim3(blocks), dim3(256), 0, c->stream, k); break;
-        case 2: hipLaunchKernelGGL((k4_trace<true, 4, false>), dim3(blocks), dim3(256), 0, c->stream, k); break;
-        default: hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES>), dim3(blocks), dim3(256), 0, c->stream, k);
+    // O32 instantiations need every level below 4 GiB: n <= 512
+    const bool o32 = g.n <= 512;
+#define VCT_K4(BRICK, MINW, UNION)                                                                      \
+    do {                                                                                               \
+        if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true>), dim3(blocks), dim3(256), 0, c->stream, k); \
+        else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false>), dim3(blocks), dim3(256), 0, c->stream, k);    \
+    } while (0)
+    switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers; 2 bricks without the four-face union
+        case 1: VCT_K4(false, 1, true); break;
+        case 2: VCT_K4(true, VCT_K4_MIN_WAVES, false); break;
+        case 3: VCT_K4(true, 1, true); break;
+        case 4: VCT_K4(true, 5, true); break;
+        case 5: hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, false>), dim3(blocks), dim3(256), 0, c->stream, k); break;
+        default: VCT_K4(true, VCT_K4_MIN_WAVES, true);
     }
+#undef VCT_K4
     return hipGetLastError();
 }
 
