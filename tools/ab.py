@@ -25,13 +25,15 @@ def main():
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--gbuffer", default="scene")
     ap.add_argument("--scene", default="atrium")
+    ap.add_argument("--nd", type=int, default=9, help="diffuse cones (0, 1, 9, 16)")
+    ap.add_argument("--spec", type=int, default=1, help="specular cone on/off")
     a = ap.parse_args()
     import torch
     from vct import Context, scenes
     from vct.camera import Camera
     variants = [int(v, 0) for v in a.variants.split(",")]
     g0, E = scenes.grid_for_unit_box(a.n)
-    ctx = Context(a.n, g0, E)
+    ctx = Context(a.n, g0, E, n_diffuse=a.nd, specular=bool(a.spec))
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream.cuda_stream)
     ctx.voxelize(*scenes.SCENES[a.scene]().arrays())

@@ -137,6 +137,13 @@ vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
     if (e == hipSuccess) e = hipMalloc(&g.normal, nv * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&g.occ_bits, (nv / 64) * 8);
     if (e == hipSuccess) e = hipMalloc((void**)&g.accum, nv * 64);
+    if (e == hipSuccess) {
+        StepRow rows[kMaxStepRows];
+        const float tau_d = cfg->n_diffuse == 16 ? VCT_TAN20 : VCT_TAN30;
+        if (build_step_table(tau_d, g.n, g.L, rows) < 0) e = hipErrorInvalidValue;
+        if (e == hipSuccess) e = hipMalloc((void**)&c->step_tab, sizeof rows);
+        if (e == hipSuccess) e = hipMemcpy(c->step_tab, rows, sizeof rows, hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
         vct_destroy(c);
         return e == hipErrorOutOfMemory ? VCT_ENOMEM : VCT_EDEVICE;
@@ -157,6 +164,7 @@ void vct_destroy(vct_ctx* c) {
     if (g.occ_bits) (void)hipFree(g.occ_bits);
     if (g.accum) (void)hipFree(g.accum);
     if (c->mesh.tri) (void)hipFree(c->mesh.tri);
+    if (c->step_tab) (void)hipFree(c->step_tab);
     for (auto& s : c->scratch)
         if (s.p) (void)hipFree(s.p);
     delete c;

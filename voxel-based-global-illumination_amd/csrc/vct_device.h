@@ -13,11 +13,22 @@ namespace vct {
 
 constexpr int kMaxLevels = 11;  // n <= 1024 -> L <= 10
 
-// A.6 mip level m = log2(D), D >= 1 (vct_spec.h VCT_LOG2_*).
-__device__ __forceinline__ float spec_log2(float x) {
-    uint32_t bits = __float_as_uint(x);
+// One step of a cone march with a wave-uniform aperture (A.6): every lane of
+// a cone starts at t = 1 and advances by D/2, so (t, D, l0, fr) depend only on
+// the step index.  K4 reads them from a per-context table for the diffuse
+// cones instead of re-deriving log2 per lane and step.
+struct StepRow {
+    float t, D, fr;
+    int l0;
+};
+constexpr int kMaxStepRows = 64;   // tan(20 deg) at n = 1024 needs 26 (+1 sentinel)
+
+// A.6 mip level m = log2(D), D >= 1 (vct_spec.h VCT_LOG2_*).  Host and device:
+// the host builds K4's step table with it (vct_trace.hip build_step_table).
+__host__ __device__ __forceinline__ float spec_log2(float x) {
+    uint32_t bits = __builtin_bit_cast(uint32_t, x);
     int e = (int)((bits >> 23) & 0xffu) - 127;
-    float f = __uint_as_float((bits & 0x007fffffu) | 0x3f800000u);
+    float f = __builtin_bit_cast(float, (bits & 0x007fffffu) | 0x3f800000u);
     if (f > VCT_LOG2_SQRT2) { f = f * 0.5f; e += 1; }
     float s = (f - 1.0f) / (f + 1.0f);
     float z = s * s;

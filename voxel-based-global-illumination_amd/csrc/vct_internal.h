@@ -49,6 +49,7 @@ struct vct_ctx {
     vct::Grid grid;
     vct::Mesh mesh;
     vct::Scratch scratch[4];      // reusable scratch (trace host staging, voxelize temps)
+    vct::StepRow* step_tab = nullptr;   // [kMaxStepRows] diffuse-cone step table (device)
     std::string err;
 };
 
@@ -71,6 +72,11 @@ hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_
                           float4* pos, float4* nrm, float4* alb);
 
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world);
+
+// K4 step table for aperture tau on an n^3 grid (rows until t > n*sqrt(3), then
+// one sentinel row with t = +inf); returns the row count incl. the sentinel, or
+// -1 if it exceeds kMaxStepRows
+int build_step_table(float tau, uint32_t n, uint32_t L, StepRow* rows);
 
 // scratch helper: grows scratch slot `i` to at least `bytes`
 hipError_t scratch_get(vct_ctx* c, int i, size_t bytes, void** out);

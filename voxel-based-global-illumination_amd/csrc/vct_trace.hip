@@ -106,6 +106,7 @@ struct TraceK {
     int tiles_x, rank, world, compact;
     int nd, spec_on, aniso;
     float tau_d;
+    const StepRow* steps_tab;    // diffuse-cone step table (tau_d), sentinel-terminated
 };
 
 __device__ __forceinline__ const float (*cone_table(int nd))[4] {
@@ -516,11 +517,20 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     return activeB ? blend(sA, sB, fr) : sA;
 }
 
-// one cone, wave-synchronous (A.6); same arithmetic as march()
-template <bool O32, bool UNION>
+// The step table held in registers: lane j keeps row j; row i is read with
+// v_readlane (no memory round trip at the head of every step).
+struct StepRegs {
+    float t, D, fr;
+    int l0;
+};
+
+// one cone, wave-synchronous (A.6); same arithmetic as march().  TAB: the
+// aperture is the diffuse one, (t, D, l0, fr) come from the step table.
+template <bool O32, bool UNION, bool TAB>
 __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, float ox, float oy, float oz,
                                                 float dx, float dy, float dz, float tau, float4& res,
-                                                uint32_t& texels, float4* __restrict__ lds, PhaseClock& pc) {
+                                                uint32_t& texels, float4* __restrict__ lds, const StepRegs& tab,
+                                                PhaseClock& pc) {
     const float tau2 = 2.0f * tau;
     const float nf = (float)k.n, Lf = (float)k.L;
     const int fx = dx >= 0.0f ? VCT_FACE_PX : VCT_FACE_NX;
@@ -558,27 +568,35 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     }
     BrickCache bc;
     bc.e0 = bc.e1 = BrickEntry{-1, 0, 0, 0};
-    for (;;) {
-        const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
-        if (active) {
-            if (!(a < VCT_ALPHA_STOP)) active = false;
-            else if (!(t <= k.tmax)) active = false;
-            else if (!(qx >= 0.0f && qx <= nf && qy >= 0.0f && qy <= nf && qz >= 0.0f && qz <= nf)) active = false;
+    for (int i = 0;; ++i) {
+        float D, fr;
+        int l0;
+        if constexpr (TAB) {                    // wave-uniform row i
+            t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tab.t), i));
+            D = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tab.D), i));
+            fr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tab.fr), i));
+            l0 = __builtin_amdgcn_readlane(tab.l0, i);
         }
+        const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
+        // a >= 0.95, t > tmax or outside the grid ends the lane's march (no short-circuit branches)
+        const bool inside = (qx >= 0.0f) & (qx <= nf) & (qy >= 0.0f) & (qy <= nf) & (qz >= 0.0f) & (qz <= nf);
+        active = active & (a < VCT_ALPHA_STOP) & (t <= k.tmax) & inside;
         const unsigned long long am = __ballot(active);
         if (am == 0ull) break;
-        const float D = fmaxf(1.0f, tau2 * t);
-        float m = spec_log2(D);
-        if (m > Lf) m = Lf;
-        const int l0 = (int)m;
-        const float fr = m - (float)l0;
+        if constexpr (!TAB) {
+            D = fmaxf(1.0f, tau2 * t);
+            float m = spec_log2(D);
+            if (m > Lf) m = Lf;
+            l0 = (int)m;
+            fr = m - (float)l0;
+        }
         const bool two = fr > 0.0f && l0 < k.L;
-        const int l0f = __builtin_amdgcn_readlane(l0, __builtin_ctzll(am));
+        const int l0f = TAB ? l0 : __builtin_amdgcn_readlane(l0, __builtin_ctzll(am));
         float4 s;
-        if (__all(!active || l0 == l0f)) {     // wave-uniform mip pair: brick path
+        if (TAB || __all(!active || l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
-            s = step_bricks<O32, UNION>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy, wdz,
-                                   lds, bc, pc);
+            s = step_bricks<O32, UNION>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy,
+                                        wdz, lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
             s = sample_level<O32>(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
             if (two) s = blend(s, sample_level<O32>(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz), fr);
@@ -591,7 +609,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
             cg = fmaf(oma, s.y, cg);
             cb = fmaf(oma, s.z, cb);
             a = fmaf(oma, s.w, a);
-            t = t + VCT_STEP_SCALE * D;
+            if constexpr (!TAB) t = t + VCT_STEP_SCALE * D;
             ++steps;
         }
         pc.mark(5);
@@ -632,6 +650,11 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
     // BRICK: every lane of a wave with any valid pixel stays in the wave-uniform
     // loops (background lanes stage texels); variant 1: only valid lanes trace
     const bool run = BRICK ? __any(valid) : valid;
+    StepRegs tab{};
+    if (BRICK && run && lane < (uint32_t)kMaxStepRows) {
+        const StepRow r = k.steps_tab[lane];
+        tab = StepRegs{r.t, r.D, r.fr, r.l0};
+    }
     if (run) {
         float4 N4 = make_float4(0.0f, 1.0f, 0.0f, 0.0f);
         if (valid) N4 = k.nrm[pix];
@@ -653,7 +676,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             const float dy = (cn * ny + ct * Ty) + cb * By;
             const float dz = (cn * nz + ct * Tz) + cb * Bz;
             float4 res;
-            if constexpr (BRICK) steps += march_brick<O32, UNION>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, pc);
+            if constexpr (BRICK) steps += march_brick<O32, UNION, true>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, tab, pc);
             else steps += march<O32>(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
             ir = fmaf(wk, res.x, ir);
             ig = fmaf(wk, res.y, ig);
@@ -673,7 +696,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             if (valid) rough = k.alb[pix].w;
             const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
             float4 res;
-            if constexpr (BRICK) steps += march_brick<O32, UNION>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, pc);
+            if constexpr (BRICK) steps += march_brick<O32, UNION, false>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
             else steps += march<O32>(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
             sout = sel4(valid, res, sout);
         }
@@ -695,6 +718,25 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
 }
 
 }  // namespace
+
+int build_step_table(float tau, uint32_t n, uint32_t L, StepRow* rows) {
+    // the march() recurrence of the kernels, on the host (same binary32 operation sequence)
+    const float tau2 = 2.0f * tau, tmax = (float)n * VCT_SQRT3, Lf = (float)L;
+    float t = 1.0f;
+    for (int i = 0; i < kMaxStepRows; ++i) {
+        if (!(t <= tmax)) {
+            rows[i] = StepRow{__builtin_huge_valf(), 1.0f, 0.0f, 0};
+            return i + 1;
+        }
+        const float D = fmaxf(1.0f, tau2 * t);
+        float m = spec_log2(D);
+        if (m > Lf) m = Lf;
+        const int l0 = (int)m;
+        rows[i] = StepRow{t, D, m - (float)l0, l0};
+        t = t + VCT_STEP_SCALE * D;
+    }
+    return -1;
+}
 
 hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     const Grid& g = c->grid;
@@ -719,6 +761,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.spec_on = c->cfg.specular ? 1 : 0;
     k.aniso = g.aniso;
     k.tau_d = c->cfg.n_diffuse == 16 ? VCT_TAN20 : VCT_TAN30;
+    k.steps_tab = c->step_tab;
     const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
     const uint32_t blocks = nlt * 16;
