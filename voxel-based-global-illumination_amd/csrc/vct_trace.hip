@@ -131,7 +131,7 @@ __device__ __forceinline__ float4 combine3(float wx, float wy, float wz, float4 
 }
 
 // corners whose three anisotropic faces are in registers at once (VGPR budget)
-constexpr int kCh = 2;
+constexpr int kCh = 4;
 
 // trilinear corner weights (x fastest), w_c = (wx * wy) * wz
 __device__ __forceinline__ void corner_weights(float fx, float fy, float fz, float (&wc)[8]) {
