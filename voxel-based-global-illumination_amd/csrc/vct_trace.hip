@@ -113,6 +113,12 @@ __device__ __forceinline__ const float (*cone_table(int nd))[4] {
     return nd == 16 ? c_cones16 : (nd == 9 ? c_cones9 : c_cones1);
 }
 
+// Wave votes on lane masks (SGPR pairs).  HIP's __any/__all/__ballot take an
+// int and round-trip every predicate through a VGPR (v_cndmask + v_cmp).
+__device__ __forceinline__ unsigned long long wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool wany(bool p) { return wballot(p) != 0ull; }
+__device__ __forceinline__ bool wall(bool p) { return wballot(!p) == 0ull; }
+
 __device__ __forceinline__ float4 sel4(bool c, float4 a, float4 b) {   // a float4 `?:` lowers to scratch
     return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
@@ -321,7 +327,7 @@ __device__ __forceinline__ Corner level_corner(int l, float qx, float qy, float 
 }
 
 __device__ __forceinline__ bool in_brick(const Corner& c, const BrickEntry& b) {
-    return (uint32_t)(c.ix - b.ox) <= 2u && (uint32_t)(c.iy - b.oy) <= 2u && (uint32_t)(c.iz - b.oz) <= 2u;
+    return max(max((uint32_t)(c.ix - b.ox), (uint32_t)(c.iy - b.oy)), (uint32_t)(c.iz - b.oz)) <= 2u;
 }
 
 // Brick origin on one axis without a 64-lane reduction: relative to the first
@@ -330,17 +336,18 @@ __device__ __forceinline__ bool in_brick(const Corner& c, const BrickEntry& b) {
 __device__ __forceinline__ int wave_origin(int v, bool active, int fl) {
     const int b = __builtin_amdgcn_readlane(v, fl);
     const int d = v - b;
-    return b + (__any(active && d < -1) ? -2 : (__any(active && d < 0) ? -1 : 0));
+    const unsigned long long m2 = wballot(active & (d < -1)), m1 = wballot(active & (d < 0));
+    return b + (m2 ? -2 : (m1 ? -1 : 0));
 }
 
 // the per-axis minimum corner over the active lanes, if every footprint fits the brick there
 __device__ __forceinline__ bool brick_origin(const Corner& c, bool active, BrickEntry& b) {
-    const unsigned long long am = __ballot(active);
+    const unsigned long long am = wballot(active);
     const int fl = am ? __builtin_ctzll(am) : 0;
     b.ox = wave_origin(c.ix, active, fl);
     b.oy = wave_origin(c.iy, active, fl);
     b.oz = wave_origin(c.iz, active, fl);
-    return __all(!active || in_brick(c, b));
+    return wall(!active | in_brick(c, b));
 }
 
 enum { kIso = 0, kComb = 1, kFaces = 2 };
@@ -443,7 +450,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
                                               float4* __restrict__ lds, BrickCache& bc, PhaseClock& pc) {
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const bool activeB = active && two;
-    const bool needB = __any(activeB);
+    const bool needB = wany(activeB);
     const int l1 = l0 + 1;                     // needB implies l0 < L
     const int aniso_mode = cc.dir_uniform ? kComb : kFaces;
     const int modeA = (l0 == 0 || !k.aniso) ? kIso : aniso_mode;
@@ -455,7 +462,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // level A: cached, restaged, or gathered
     const Corner cA = level_corner(l0, qx, qy, qz);
     BrickEntry bA = bc.get(eA);
-    bool useA = bA.lvl == l0 && __all(!active || in_brick(cA, bA));
+    bool useA = bA.lvl == l0 && wall(!active | in_brick(cA, bA));
     bool stA = false;
     if (!useA && (modeA != kFaces || faces_ok)) {
         BrickEntry nb;
@@ -471,7 +478,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     bool useB = false, stB = false;
     if (needB) {
         cB = level_corner(l1, qx, qy, qz);
-        useB = bB.lvl == l1 && __all(!activeB || in_brick(cB, bB));
+        useB = bB.lvl == l1 && wall(!activeB | in_brick(cB, bB));
         if (!useB && (modeB != kFaces || faces_ok)) {
             BrickEntry nb;
             nb.lvl = l1;
@@ -543,11 +550,11 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     ConeCtl cc;
     int bx, by, bz;              // this lane's face blocks in a faces-mode brick (float4 offsets)
     {
-        const unsigned long long vm = __ballot(valid);
+        const unsigned long long vm = wballot(valid);
         const int fl = vm ? __builtin_ctzll(vm) : 0;
         int u = 0;
 #pragma unroll
-        for (int f = 0; f < 6; ++f) u |= __any(valid && (fx == f || fy == f || fz == f)) ? 1 << f : 0;
+        for (int f = 0; f < 6; ++f) u |= wany(valid & ((fx == f) | (fy == f) | (fz == f))) ? 1 << f : 0;
         cc.funion = u;
         cc.nfaces = __builtin_popcount(u);
         cc.f0 = __builtin_ctz(u | 64);
@@ -564,7 +571,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.uwy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdy), fl));
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
         // same d^2 everywhere AND one face per axis (d and -d share d^2)
-        cc.dir_uniform = __all(!valid || (wdx == cc.uwx && wdy == cc.uwy && wdz == cc.uwz)) && cc.nfaces == 3;
+        cc.dir_uniform = wall(!valid | ((wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz))) && cc.nfaces == 3;
     }
     BrickCache bc;
     bc.e0 = bc.e1 = BrickEntry{-1, 0, 0, 0};
@@ -581,7 +588,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         // a >= 0.95, t > tmax or outside the grid ends the lane's march (no short-circuit branches)
         const bool inside = (qx >= 0.0f) & (qx <= nf) & (qy >= 0.0f) & (qy <= nf) & (qz >= 0.0f) & (qz <= nf);
         active = active & (a < VCT_ALPHA_STOP) & (t <= k.tmax) & inside;
-        const unsigned long long am = __ballot(active);
+        const unsigned long long am = wballot(active);
         if (am == 0ull) break;
         if constexpr (!TAB) {
             D = fmaxf(1.0f, tau2 * t);
@@ -593,7 +600,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         const bool two = fr > 0.0f && l0 < k.L;
         const int l0f = TAB ? l0 : __builtin_amdgcn_readlane(l0, __builtin_ctzll(am));
         float4 s;
-        if (TAB || __all(!active || l0 == l0f)) {     // wave-uniform mip pair: brick path
+        if (TAB || wall(!active | (l0 == l0f))) {     // wave-uniform mip pair: brick path
             pc.mark(0);
             s = step_bricks<O32, UNION>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy,
                                         wdz, lds, bc, pc);
@@ -649,7 +656,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
     const bool valid = P.w != 0.0f;
     // BRICK: every lane of a wave with any valid pixel stays in the wave-uniform
     // loops (background lanes stage texels); variant 1: only valid lanes trace
-    const bool run = BRICK ? __any(valid) : valid;
+    const bool run = BRICK ? wany(valid) : valid;
     StepRegs tab{};
     if (BRICK && run && lane < (uint32_t)kMaxStepRows) {
         const StepRow r = k.steps_tab[lane];
