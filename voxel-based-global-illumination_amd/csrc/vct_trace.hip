@@ -114,10 +114,14 @@ __device__ __forceinline__ const float (*cone_table(int nd))[4] {
 }
 
 // Wave votes on lane masks (SGPR pairs).  HIP's __any/__all/__ballot take an
-// int and round-trip every predicate through a VGPR (v_cndmask + v_cmp).
+// int and round-trip every predicate through a VGPR (v_cndmask + v_cmp); so
+// does a ballot of an ANDed predicate.  Vote on the bare compare and AND the
+// lane set in as a scalar mask: ballot(c) & m.
 __device__ __forceinline__ unsigned long long wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ bool wany(bool p) { return wballot(p) != 0ull; }
 __device__ __forceinline__ bool wall(bool p) { return wballot(!p) == 0ull; }
+// every lane of mask m satisfies c
+__device__ __forceinline__ bool wall_in(unsigned long long m, bool c) { return (wballot(!c) & m) == 0ull; }
 
 __device__ __forceinline__ float4 sel4(bool c, float4 a, float4 b) {   // a float4 `?:` lowers to scratch
     return make_float4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
@@ -146,21 +150,55 @@ __device__ __forceinline__ void corner_weights(float fx, float fy, float fz, flo
     for (int c = 0; c < 8; ++c) wc[c] = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
 }
 
-// A texel by index within a level.  O32 (every level < 4 GiB, n <= 512): a
-// 32-bit byte offset from the wave-uniform level base, so the load is
-// global_load with an SGPR base and ONE offset VGPR; else 64-bit addresses.
+// One level of the pyramid as the kernels read it.  O32 (every level below
+// 2 GiB, n <= 512): a buffer resource over the level (wave-uniform, SGPRs),
+// 32-bit byte offsets, and the spec's zero border from the hardware range
+// check -- a texel outside the level is fetched at an out-of-range offset and
+// reads as 0, so no select waits on the load.  Else: 64-bit addresses and an
+// explicit select.
 template <bool O32>
-__device__ __forceinline__ float4 texel(const float4* __restrict__ lvl, uint32_t i) {
-    if constexpr (O32) return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(lvl) + (i << 4));
-    else return lvl[i];
+struct LevelView;
+
+template <>
+struct LevelView<true> {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ float4 fetch(uint32_t i, bool in) const {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, in ? i << 4 : 0xfffffff0u, 0, 0);
+        return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+};
+
+template <>
+struct LevelView<false> {
+    const float4* p;
+    __device__ float4 fetch(uint32_t i, bool in) const {
+        const float4 v = p[in ? i : 0u];
+        return sel4(in, v, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    }
+};
+
+// level l (wave-uniform): O32 derives the offset in closed form on the scalar
+// unit (sum of (n >> j)^3 over j = 1 .. l-1 = (n^3 - (n >> (l-1))^3) / 7)
+template <bool O32>
+__device__ __forceinline__ LevelView<O32> level_view(const TraceK& k, int l) {
+    if constexpr (O32) {
+        const uint32_t n = (uint32_t)k.n, n3 = n * n * n, F = k.aniso ? 6u : 1u;
+        const uint32_t m = n >> (l > 0 ? l - 1 : 0), nl = n >> l;
+        const uint32_t off = l == 0 ? 0u : n3 + F * ((n3 - m * m * m) / 7u);
+        const uint32_t bytes = (l == 0 ? 1u : F) * nl * nl * nl * 16u;
+        return LevelView<true>{__builtin_amdgcn_make_buffer_rsrc((void*)(k.pyr + off), (short)0, (int)bytes,
+                                                                 0x00020000)};
+    } else {
+        return LevelView<false>{k.pyr + k.lvl_off[l]};
+    }
 }
 
 // ===========================================================================
 // per-lane gathers (variant 1, and the fallback of variant 0)
 // ===========================================================================
 // D_l(q, d) (A.5): level 0 / isotropic = T_l; anisotropic = faces combined per
-// corner texel, then trilinear.  Zero border: out-of-range corners get weight 0
-// on a clamped (valid) address; fmaf(0, v, acc) == acc for the finite texels.
+// corner texel, then trilinear.  Zero border: out-of-range corners read as 0
+// (LevelView); fmaf(w, 0, acc) == acc, the spec's zero-border sum.
 template <bool O32>
 __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx, float qy, float qz,
                                                int fx, int fy, int fz, float wdx, float wdy, float wdz) {
@@ -172,20 +210,20 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
     float wc[8];
     corner_weights(cx - flx, cy - fly, cz - flz, wc);
     uint32_t idx[8];
+    bool in[8];
     const int xs[2] = {ix, ix + 1}, ys[2] = {iy, iy + 1}, zs[2] = {iz, iz + 1};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         const int x = xs[c & 1], y = ys[(c >> 1) & 1], z = zs[c >> 2];
-        const bool in = (unsigned)x < (unsigned)nl && (unsigned)y < (unsigned)nl && (unsigned)z < (unsigned)nl;
-        idx[c] = in ? (uint32_t)x + (uint32_t)nl * ((uint32_t)y + (uint32_t)nl * (uint32_t)z) : 0u;
-        wc[c] = in ? wc[c] : 0.0f;
+        in[c] = (unsigned)x < (unsigned)nl && (unsigned)y < (unsigned)nl && (unsigned)z < (unsigned)nl;
+        idx[c] = (uint32_t)x + (uint32_t)nl * ((uint32_t)y + (uint32_t)nl * (uint32_t)z);
     }
-    const float4* lvl = k.pyr + k.lvl_off[l];
+    const LevelView<O32> lv = level_view<O32>(k, l);
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (l == 0 || !k.aniso) {
         float4 v[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = texel<O32>(lvl, idx[c]);
+        for (int c = 0; c < 8; ++c) v[c] = lv.fetch(idx[c], in[c]);
 #pragma unroll
         for (int c = 0; c < 8; ++c) acc_fma(acc, wc[c], v[c]);
         return acc;
@@ -197,9 +235,9 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
         float4 vx[kCh], vy[kCh], vz[kCh];
 #pragma unroll
         for (int c = 0; c < kCh; ++c) {
-            vx[c] = texel<O32>(lvl, X + idx[h + c]);
-            vy[c] = texel<O32>(lvl, Y + idx[h + c]);
-            vz[c] = texel<O32>(lvl, Z + idx[h + c]);
+            vx[c] = lv.fetch(X + idx[h + c], in[h + c]);
+            vy[c] = lv.fetch(Y + idx[h + c], in[h + c]);
+            vz[c] = lv.fetch(Z + idx[h + c], in[h + c]);
         }
 #pragma unroll
         for (int c = 0; c < kCh; ++c) acc_fma(acc, wc[h + c], combine3(wdx, wdy, wdz, vx[c], vy[c], vz[c]));
@@ -333,21 +371,20 @@ __device__ __forceinline__ bool in_brick(const Corner& c, const BrickEntry& b) {
 // Brick origin on one axis without a 64-lane reduction: relative to the first
 // active lane's corner b, the wave fits only if every active lane is within
 // [b-2, b+2]; two ballots then give the minimum exactly (-2, -1 or 0).
-__device__ __forceinline__ int wave_origin(int v, bool active, int fl) {
+__device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl) {
     const int b = __builtin_amdgcn_readlane(v, fl);
     const int d = v - b;
-    const unsigned long long m2 = wballot(active & (d < -1)), m1 = wballot(active & (d < 0));
-    return b + (m2 ? -2 : (m1 ? -1 : 0));
+    const unsigned long long m2 = wballot(d < -1) & am, m1 = wballot(d < 0) & am;   // m2 within m1
+    return b - (int)(m1 != 0ull) - (int)(m2 != 0ull);
 }
 
-// the per-axis minimum corner over the active lanes, if every footprint fits the brick there
-__device__ __forceinline__ bool brick_origin(const Corner& c, bool active, BrickEntry& b) {
-    const unsigned long long am = wballot(active);
+// the per-axis minimum corner over the lanes of am, if every footprint fits the brick there
+__device__ __forceinline__ bool brick_origin(const Corner& c, unsigned long long am, BrickEntry& b) {
     const int fl = am ? __builtin_ctzll(am) : 0;
-    b.ox = wave_origin(c.ix, active, fl);
-    b.oy = wave_origin(c.iy, active, fl);
-    b.oz = wave_origin(c.iz, active, fl);
-    return wall(!active | in_brick(c, b));
+    b.ox = wave_origin(c.ix, am, fl);
+    b.oy = wave_origin(c.iy, am, fl);
+    b.oz = wave_origin(c.iz, am, fl);
+    return wall_in(am, in_brick(c, b));
 }
 
 enum { kIso = 0, kComb = 1, kFaces = 2 };
@@ -362,19 +399,19 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
     const int lane = threadIdx.x & 63;
     const int sx = be.ox + (lane & 3), sy = be.oy + ((lane >> 2) & 3), sz = be.oz + (lane >> 4);
     const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
-    const uint32_t gi = inb ? (uint32_t)sx + (uint32_t)nl * ((uint32_t)sy + (uint32_t)nl * (uint32_t)sz) : 0u;
+    const uint32_t gi = (uint32_t)sx + (uint32_t)nl * ((uint32_t)sy + (uint32_t)nl * (uint32_t)sz);
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const float4* lvl = k.pyr + k.lvl_off[l];
+    const LevelView<O32> lv = level_view<O32>(k, l);
     Tex4 t;
     t.b = t.c = t.d = z4;
     if (mode == kIso) {
-        t.a = sel4(inb, texel<O32>(lvl, gi), z4);
+        t.a = lv.fetch(gi, inb);
     } else {
         const uint32_t vl = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
-        t.a = sel4(inb, texel<O32>(lvl, (uint32_t)cc.f0 * vl + gi), z4);
-        t.b = sel4(inb, texel<O32>(lvl, (uint32_t)cc.f1 * vl + gi), z4);
-        t.c = sel4(inb, texel<O32>(lvl, (uint32_t)cc.f2 * vl + gi), z4);
-        if (cc.nfaces > 3) t.d = sel4(inb, texel<O32>(lvl, (uint32_t)cc.f3 * vl + gi), z4);
+        t.a = lv.fetch((uint32_t)cc.f0 * vl + gi, inb);
+        t.b = lv.fetch((uint32_t)cc.f1 * vl + gi, inb);
+        t.c = lv.fetch((uint32_t)cc.f2 * vl + gi, inb);
+        if (cc.nfaces > 3) t.d = lv.fetch((uint32_t)cc.f3 * vl + gi, inb);
     }
     return t;
 }
@@ -450,7 +487,8 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
                                               float4* __restrict__ lds, BrickCache& bc, PhaseClock& pc) {
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const bool activeB = active && two;
-    const bool needB = wany(activeB);
+    const unsigned long long amA = wballot(active), amB = wballot(activeB);
+    const bool needB = amB != 0ull;
     const int l1 = l0 + 1;                     // needB implies l0 < L
     const int aniso_mode = cc.dir_uniform ? kComb : kFaces;
     const int modeA = (l0 == 0 || !k.aniso) ? kIso : aniso_mode;
@@ -462,12 +500,12 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // level A: cached, restaged, or gathered
     const Corner cA = level_corner(l0, qx, qy, qz);
     BrickEntry bA = bc.get(eA);
-    bool useA = bA.lvl == l0 && wall(!active | in_brick(cA, bA));
+    bool useA = bA.lvl == l0 && wall_in(amA, in_brick(cA, bA));
     bool stA = false;
     if (!useA && (modeA != kFaces || faces_ok)) {
         BrickEntry nb;
         nb.lvl = l0;
-        if (brick_origin(cA, active, nb)) {
+        if (brick_origin(cA, amA, nb)) {
             bA = nb;
             bc.set(eA, nb);
             useA = stA = true;
@@ -478,11 +516,11 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     bool useB = false, stB = false;
     if (needB) {
         cB = level_corner(l1, qx, qy, qz);
-        useB = bB.lvl == l1 && wall(!activeB | in_brick(cB, bB));
+        useB = bB.lvl == l1 && wall_in(amB, in_brick(cB, bB));
         if (!useB && (modeB != kFaces || faces_ok)) {
             BrickEntry nb;
             nb.lvl = l1;
-            if (brick_origin(cB, activeB, nb)) {
+            if (brick_origin(cB, amB, nb)) {
                 bB = nb;
                 bc.set(eB, nb);
                 useB = stB = true;
@@ -554,7 +592,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         const int fl = vm ? __builtin_ctzll(vm) : 0;
         int u = 0;
 #pragma unroll
-        for (int f = 0; f < 6; ++f) u |= wany(valid & ((fx == f) | (fy == f) | (fz == f))) ? 1 << f : 0;
+        for (int f = 0; f < 6; ++f) u |= (wballot((fx == f) | (fy == f) | (fz == f)) & vm) ? 1 << f : 0;
         cc.funion = u;
         cc.nfaces = __builtin_popcount(u);
         cc.f0 = __builtin_ctz(u | 64);
@@ -571,7 +609,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.uwy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdy), fl));
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
         // same d^2 everywhere AND one face per axis (d and -d share d^2)
-        cc.dir_uniform = wall(!valid | ((wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz))) && cc.nfaces == 3;
+        cc.dir_uniform = wall_in(vm, (wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz)) && cc.nfaces == 3;
     }
     BrickCache bc;
     bc.e0 = bc.e1 = BrickEntry{-1, 0, 0, 0};
@@ -600,7 +638,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         const bool two = fr > 0.0f && l0 < k.L;
         const int l0f = TAB ? l0 : __builtin_amdgcn_readlane(l0, __builtin_ctzll(am));
         float4 s;
-        if (TAB || wall(!active | (l0 == l0f))) {     // wave-uniform mip pair: brick path
+        if (TAB || wall_in(am, l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
             s = step_bricks<O32, UNION>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy,
                                         wdz, lds, bc, pc);
