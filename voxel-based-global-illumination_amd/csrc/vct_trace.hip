@@ -432,6 +432,7 @@ __device__ __forceinline__ void stage_store(int mode, const ConeCtl& cc, const T
 
 // D_l from a staged brick: corner 0 at `b`; faces mode reads the lane's own
 // face blocks at float4 offsets bx, by, bz
+template <int KL>   // corners x 3 faces per LDS burst in faces mode
 __device__ __forceinline__ float4 brick_sample(const Corner& c, const BrickEntry& be, bool one_slot, int bx,
                                                int by, int bz, float wdx, float wdy, float wdz,
                                                const float4* __restrict__ lds) {
@@ -448,15 +449,15 @@ __device__ __forceinline__ float4 brick_sample(const Corner& c, const BrickEntry
     } else {
         const float4 *X = b + bx, *Y = b + by, *Z = b + bz;
 #pragma unroll
-        for (int h = 0; h < 8; h += kCh) {
-            float4 vx[kCh], vy[kCh], vz[kCh];
+        for (int h = 0; h < 8; h += KL) {
+            float4 vx[KL], vy[KL], vz[KL];
 #pragma unroll
-            for (int i = 0; i < kCh; ++i) {
+            for (int i = 0; i < KL; ++i) {
                 const int o = ((h + i) & 1) + 4 * (((h + i) >> 1) & 1) + 16 * ((h + i) >> 2);
                 vx[i] = X[o]; vy[i] = Y[o]; vz[i] = Z[o];
             }
 #pragma unroll
-            for (int i = 0; i < kCh; ++i) acc_fma(acc, wc[h + i], combine3(wdx, wdy, wdz, vx[i], vy[i], vz[i]));
+            for (int i = 0; i < KL; ++i) acc_fma(acc, wc[h + i], combine3(wdx, wdy, wdz, vx[i], vy[i], vz[i]));
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -480,7 +481,7 @@ __device__ __forceinline__ void dbg_fallback_reason(const Corner& c, bool active
 // One step's blended sample (1 - fr) D_{l0} + fr D_{l0+1} for a wave-uniform l0.
 // Each level is served from the cache, restaged (both levels' loads in one
 // batch) or, when the wave's footprint does not fit, gathered per lane.
-template <bool O32, bool UNION>
+template <bool O32, bool UNION, int KL>
 __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx, float qy, float qz, bool active,
                                               bool two, float fr, const ConeCtl& cc, int fx, int fy, int fz, int bx,
                                               int by, int bz, float wdx, float wdy, float wdz,
@@ -543,8 +544,8 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     pc.mark(2);
     float4 sA = z4, sB = z4;
     if (useA || useB) {
-        if (useA && active) sA = brick_sample(cA, bA, modeA != kFaces, bx, by, bz, wdx, wdy, wdz, ldsA);
-        if (useB && activeB) sB = brick_sample(cB, bB, modeB != kFaces, bx, by, bz, wdx, wdy, wdz, ldsB);
+        if (useA && active) sA = brick_sample<KL>(cA, bA, modeA != kFaces, bx, by, bz, wdx, wdy, wdz, ldsA);
+        if (useB && activeB) sB = brick_sample<KL>(cB, bB, modeB != kFaces, bx, by, bz, wdx, wdy, wdz, ldsB);
         wave_lds_sync();
     }
     pc.mark(3);
@@ -571,7 +572,7 @@ struct StepRegs {
 
 // one cone, wave-synchronous (A.6); same arithmetic as march().  TAB: the
 // aperture is the diffuse one, (t, D, l0, fr) come from the step table.
-template <bool O32, bool UNION, bool TAB>
+template <bool O32, bool UNION, bool TAB, int KL>
 __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, float ox, float oy, float oz,
                                                 float dx, float dy, float dz, float tau, float4& res,
                                                 uint32_t& texels, float4* __restrict__ lds, const StepRegs& tab,
@@ -640,7 +641,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         float4 s;
         if (TAB || wall_in(am, l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
-            s = step_bricks<O32, UNION>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy,
+            s = step_bricks<O32, UNION, KL>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy,
                                         wdz, lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
             s = sample_level<O32>(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
@@ -666,7 +667,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
 // ===========================================================================
 // the kernel: pixel setup, cone loop, outputs (BRICK = variant 0, else 1)
 // ===========================================================================
-template <bool BRICK, int MINW, bool UNION, bool O32>
+template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2>
 __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
     __shared__ float4 lds_all[BRICK ? 4 : 1][BRICK ? 2 * kEntrySlots : 1];
     // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid
@@ -721,7 +722,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             const float dy = (cn * ny + ct * Ty) + cb * By;
             const float dz = (cn * nz + ct * Tz) + cb * Bz;
             float4 res;
-            if constexpr (BRICK) steps += march_brick<O32, UNION, true>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, tab, pc);
+            if constexpr (BRICK) steps += march_brick<O32, UNION, true, KL>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, tab, pc);
             else steps += march<O32>(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
             ir = fmaf(wk, res.x, ir);
             ig = fmaf(wk, res.y, ig);
@@ -741,7 +742,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             if (valid) rough = k.alb[pix].w;
             const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
             float4 res;
-            if constexpr (BRICK) steps += march_brick<O32, UNION, false>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
+            if constexpr (BRICK) steps += march_brick<O32, UNION, false, KL>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
             else steps += march<O32>(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
             sout = sel4(valid, res, sout);
         }
@@ -823,6 +824,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         case 3: VCT_K4(true, 1, true); break;
         case 4: VCT_K4(true, 5, true); break;
         case 5: hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, false>), dim3(blocks), dim3(256), 0, c->stream, k); break;
+        case 6: hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 1>), dim3(blocks), dim3(256), 0, c->stream, k); break;
         default: VCT_K4(true, VCT_K4_MIN_WAVES, true);
     }
 #undef VCT_K4
