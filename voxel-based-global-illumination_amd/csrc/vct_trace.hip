@@ -309,7 +309,14 @@ __device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, f
 // reuses the entry when it holds level l and every active lane's footprint
 // still lies inside it.  Consecutive steps move ~0.25-1 texel, so a brick
 // typically serves two to four steps.
-constexpr int kEntrySlots = 4 * 64;            // float4 per cache entry (up to 4 face blocks)
+// Brick layout in LDS (float4 slots): texel (x, y, z) at x + 4y + kBz z.  A
+// ds_read_b128 serves 16 lanes per LDS cycle, conflict-free when their slots
+// differ mod 16; kBz = 19 (= 3 mod 16) keeps the 3x3 corner offsets a wave
+// spans in any two axes (floors, walls) distinct mod 16, where 16 would alias
+// every z step onto the same banks.
+constexpr int kBz = 19;
+constexpr int kBlk = 3 * kBz + 16;              // one face block: 73 slots
+constexpr int kEntrySlots = 4 * kBlk;           // float4 per cache entry (up to 4 face blocks)
 
 // One wave's LDS hand-off (writes -> other lanes' reads, and reads -> next
 // writes): the asm "memory" clobber keeps the compiler from moving DS ops
@@ -418,15 +425,16 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
 
 __device__ __forceinline__ void stage_store(int mode, const ConeCtl& cc, const Tex4& t, float4* __restrict__ lds) {
     const int lane = threadIdx.x & 63;
+    float4* p = lds + ((lane & 15) + kBz * (lane >> 4));
     if (mode == kIso) {
-        lds[lane] = t.a;
+        p[0] = t.a;
     } else if (mode == kComb) {     // f0, f1, f2 = the x, y, z faces
-        lds[lane] = combine3(cc.uwx, cc.uwy, cc.uwz, t.a, t.b, t.c);
+        p[0] = combine3(cc.uwx, cc.uwy, cc.uwz, t.a, t.b, t.c);
     } else {
-        lds[lane] = t.a;
-        lds[64 + lane] = t.b;
-        lds[128 + lane] = t.c;
-        if (cc.nfaces > 3) lds[192 + lane] = t.d;
+        p[0] = t.a;
+        p[kBlk] = t.b;
+        p[2 * kBlk] = t.c;
+        if (cc.nfaces > 3) p[3 * kBlk] = t.d;
     }
 }
 
@@ -438,12 +446,12 @@ __device__ __forceinline__ float4 brick_sample(const Corner& c, const BrickEntry
                                                const float4* __restrict__ lds) {
     float wc[8];
     corner_weights(c.fx, c.fy, c.fz, wc);
-    const float4* b = lds + ((c.ix - be.ox) + 4 * (c.iy - be.oy) + 16 * (c.iz - be.oz));
+    const float4* b = lds + ((c.ix - be.ox) + 4 * (c.iy - be.oy) + kBz * (c.iz - be.oz));
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (one_slot) {
         float4 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = b[(i & 1) + 4 * ((i >> 1) & 1) + 16 * (i >> 2)];
+        for (int i = 0; i < 8; ++i) v[i] = b[(i & 1) + 4 * ((i >> 1) & 1) + kBz * (i >> 2)];
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc_fma(acc, wc[i], v[i]);
     } else {
@@ -453,7 +461,7 @@ __device__ __forceinline__ float4 brick_sample(const Corner& c, const BrickEntry
             float4 vx[KL], vy[KL], vz[KL];
 #pragma unroll
             for (int i = 0; i < KL; ++i) {
-                const int o = ((h + i) & 1) + 4 * (((h + i) >> 1) & 1) + 16 * ((h + i) >> 2);
+                const int o = ((h + i) & 1) + 4 * (((h + i) >> 1) & 1) + kBz * ((h + i) >> 2);
                 vx[i] = X[o]; vy[i] = Y[o]; vz[i] = Z[o];
             }
 #pragma unroll
@@ -603,9 +611,9 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.f2 = __builtin_ctz(u | 64);
         u &= u - 1;
         cc.f3 = __builtin_ctz(u | 64);
-        bx = 64 * __builtin_popcount(cc.funion & ((1 << fx) - 1));
-        by = 64 * __builtin_popcount(cc.funion & ((1 << fy) - 1));
-        bz = 64 * __builtin_popcount(cc.funion & ((1 << fz) - 1));
+        bx = kBlk * __builtin_popcount(cc.funion & ((1 << fx) - 1));
+        by = kBlk * __builtin_popcount(cc.funion & ((1 << fy) - 1));
+        bz = kBlk * __builtin_popcount(cc.funion & ((1 << fz) - 1));
         cc.uwx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdx), fl));
         cc.uwy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdy), fl));
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
@@ -821,10 +829,6 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers; 2 bricks without the four-face union
         case 1: VCT_K4(false, 1, true); break;
         case 2: VCT_K4(true, VCT_K4_MIN_WAVES, false); break;
-        case 3: VCT_K4(true, 1, true); break;
-        case 4: VCT_K4(true, 5, true); break;
-        case 5: hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, false>), dim3(blocks), dim3(256), 0, c->stream, k); break;
-        case 6: hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 1>), dim3(blocks), dim3(256), 0, c->stream, k); break;
         default: VCT_K4(true, VCT_K4_MIN_WAVES, true);
     }
 #undef VCT_K4
