@@ -1,0 +1,35 @@
+/* vct_host.h — C entry points of the host scene loader (host/scene.cpp).
+ *
+ * The reference loads models with assimp inside Model::loadModel
+ * (assets/code/scene/model.cpp:21-36: ReadFile with aiProcess_Triangulate |
+ * aiProcess_FlipUVs | aiProcess_CalcTangentSpace) and flattens each aiMesh into
+ * a vector<Vertex> + vector<GLuint> + Material (model.cpp:38-148).  These
+ * functions expose the same result for a Wavefront OBJ/MTL file: per mesh the
+ * 56-byte Vertex array (stdafx.h:36-42) and u32 triangle indices, and per
+ * material Ka/Kd/Ks as (r, g, b, 1) (model.cpp:48-53).  CPU only; no HIP.
+ */
+#ifndef VCT_HOST_H
+#define VCT_HOST_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vcth_model vcth_model;
+
+/* Load an OBJ (+ mtllib).  Returns 0, or -1 with a message in err (model.cpp:25-29 prints one). */
+int vcth_load_obj(const char* path, vcth_model** out, char* err, int errlen);
+uint32_t vcth_num_meshes(const vcth_model* m);
+uint32_t vcth_num_materials(const vcth_model* m);
+/* Mesh i: verts = n_verts x 56-byte Vertex, idx = n_idx u32 (triangles), material index. */
+int vcth_mesh(const vcth_model* m, uint32_t i, const void** verts, uint32_t* n_verts, const uint32_t** idx,
+              uint32_t* n_idx, uint32_t* material);
+/* Material i: name, Ka/Kd/Ks (r, g, b, 1). */
+int vcth_material(const vcth_model* m, uint32_t i, const char** name, float ka[4], float kd[4], float ks[4]);
+void vcth_free(vcth_model* m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

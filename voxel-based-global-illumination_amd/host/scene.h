@@ -7,7 +7,7 @@
 // models with assimp (model.cpp:21-148); assimp is not available on Linux in
 // this image (its vendored lib is an MSVC import library), so Model::LoadObj is
 // a small Wavefront OBJ/MTL reader covering what the VCT path consumes
-// (positions, normals, texcoords, faces triangulated as a fan, usemtl/Kd).
+// (see scene.cpp for the assimp 3.3 rules it reproduces).
 #pragma once
 #include <array>
 #include <memory>
