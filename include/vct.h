@@ -143,6 +143,18 @@ vct_status vct_gbuffer_raycast_device(vct_ctx* ctx, const vct_camera* cam, uint3
                                       uint32_t height, float roughness, float* pos4,
                                       float* nrm4, float* alb4);
 
+/* ---- composite + present -------------------------------
+ * final = direct + albedo * diffuse.rgb + spec.rgb per pixel, direct = albedo *
+ * color * max(n.l, 0) * shadow (the K2 voxel walk from the cone origin), into
+ * out_linear4 (float4, a = 1 / 0 background) and/or out_rgba8 (Reinhard, gamma
+ * 1/2.2; background = the reference's clear colour, r_voxelization.cpp:8).
+ * Device pointers: the G-buffer of the frame and vct_trace_device's outputs.
+ * Either output may be NULL, not both.  Needs vct_voxelize. */
+vct_status vct_composite_device(vct_ctx* ctx, const float* pos4, const float* nrm4, const float* alb4,
+                                const float* diffuse4, const float* spec4, uint32_t width, uint32_t height,
+                                const float dir_to_light[3], const float color[3], float* out_linear4,
+                                uint32_t* out_rgba8);
+
 /* ---- device memory for hosts without HIP headers (FFI bindings) ----------
  * kind: 0 host->device, 1 device->host, 2 device->device; synchronous. */
 vct_status vct_device_alloc(vct_ctx* ctx, size_t bytes, void** dptr);

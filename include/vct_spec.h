@@ -103,4 +103,16 @@
 /* ---- multi-GPU screen tiling ---------------------------------- */
 #define VCT_TILE            64           /* 64x64-pixel tiles, round-robin by rank */
 
+/* Composite + present:
+ *   direct = ((albedo * color) * max(n.l, 0)) * V     V: the K2 DDA shadow walk
+ *            from q = (P - g0) * n/E + N (the cone origin) toward l
+ *   final  = (direct + albedo * diffuse.rgb) + spec.rgb          (linear)
+ *   rgba8  = round(255 * (f / (1 + f))^(1/2.2)) per channel, alpha 255;
+ *            background pixels = the reference's clear colour
+ *            (glClearColor(0.2, 0.3, 0.3, 1), r_voxelization.cpp:8). */
+#define VCT_CLEAR_R         0.2f
+#define VCT_CLEAR_G         0.3f
+#define VCT_CLEAR_B         0.3f
+#define VCT_INV_GAMMA       0.454545468f /* 1 / 2.2 */
+
 #endif /* VCT_SPEC_H */

@@ -53,6 +53,8 @@ def lib():
         L.vo_trace.restype = C.c_uint64
         L.vo_trace.argtypes = [C.POINTER(_TraceParams), P, P, P, P, P, C.c_uint32, C.c_uint32, C.c_uint32,
                                P, P, P, C.c_int]
+        L.vo_composite.restype = None
+        L.vo_composite.argtypes = [C.c_uint32, P, C.c_float, P, P, P, P, P, P, C.c_uint32, C.c_uint32, P, P, P, P]
         L.vo_log2.restype = C.c_float
         L.vo_log2.argtypes = [C.c_float]
         _lib = L
@@ -140,6 +142,19 @@ def trace(n, aabb_min, extent, r0, pyr, pos4, nrm4, alb4, eye, aniso=True, n_dif
                          _p(np.ascontiguousarray(alb4, np.float32)), w, h, row_step,
                          _p(diff), _p(spec), _p(steps), threads)
     return {"diffuse": diff, "spec": spec, "steps_px": steps, "cone_steps": int(tot)}
+
+
+def composite(n, aabb_min, extent, albedo_occ, pos4, nrm4, alb4, diffuse4, spec4, dir_to_light,
+              color=(1.0, 1.0, 1.0)):
+    """f3 composite (vct_spec.h) -> (linear float4 [h][w][4], rgba8 uint32 [h][w])."""
+    h, w = pos4.shape[:2]
+    lin = np.empty((h, w, 4), np.float32)
+    rgba = np.empty((h, w), np.uint32)
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)
+    lib().vo_composite(n, _p(f32(aabb_min)), float(extent), _p(f32(albedo_occ)), _p(f32(pos4)), _p(f32(nrm4)),
+                       _p(f32(alb4)), _p(f32(diffuse4)), _p(f32(spec4)), w, h, _p(f32(dir_to_light)),
+                       _p(f32(color)), _p(lin), _p(rgba))
+    return lin, rgba
 
 
 def pipeline(n, aabb_min, extent, verts, idx, tri_mat, kd4, light_dir, light_color=(1, 1, 1), aniso=True):

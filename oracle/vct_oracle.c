@@ -237,6 +237,55 @@ void vo_inject(uint32_t n, const float* albedo_occ4, const float* normal4,
 }
 
 /* ------------------------------------------------------------------------- */
+/* f3  composite + present (vct_spec.h)                                        */
+/* ------------------------------------------------------------------------- */
+
+static uint32_t to8(float v) {
+    v = v / (1.0f + v);
+    v = powf(v < 0.0f ? 0.0f : v, VCT_INV_GAMMA);
+    long q = lroundf(v * 255.0f);
+    return (uint32_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
+}
+
+void vo_composite(uint32_t n, const float g0[3], float extent, const float* albedo_occ4,
+                  const float* pos4, const float* nrm4, const float* alb4, const float* diffuse4,
+                  const float* spec4, uint32_t w, uint32_t h, const float dir_to_light[3],
+                  const float color[3], float* out_lin4, uint32_t* out_rgba8) {
+    v3 l = {dir_to_light[0], dir_to_light[1], dir_to_light[2]};
+    float len = sqrtf(v3dot(l, l));
+    if (len > 0.0f) { l.x = l.x / len; l.y = l.y / len; l.z = l.z / len; }
+    const float inv_h = (float)n / extent;
+    for (size_t i = 0; i < (size_t)w * h; ++i) {
+        const float *P = pos4 + 4 * i, *N = nrm4 + 4 * i, *A = alb4 + 4 * i;
+        const float *D = diffuse4 + 4 * i, *S = spec4 + 4 * i;
+        if (P[3] == 0.0f) {
+            if (out_lin4) {
+                out_lin4[4 * i] = VCT_CLEAR_R; out_lin4[4 * i + 1] = VCT_CLEAR_G;
+                out_lin4[4 * i + 2] = VCT_CLEAR_B; out_lin4[4 * i + 3] = 0.0f;
+            }
+            if (out_rgba8)
+                out_rgba8[i] = (uint32_t)lroundf(VCT_CLEAR_R * 255.0f) | ((uint32_t)lroundf(VCT_CLEAR_G * 255.0f) << 8) |
+                               ((uint32_t)lroundf(VCT_CLEAR_B * 255.0f) << 16) | (255u << 24);
+            continue;
+        }
+        v3 nm = {N[0], N[1], N[2]};
+        float ndl = v3dot(nm, l);
+        float d[3] = {0.0f, 0.0f, 0.0f};
+        if (ndl > 0.0f) {
+            v3 q = {(P[0] - g0[0]) * inv_h + nm.x, (P[1] - g0[1]) * inv_h + nm.y, (P[2] - g0[2]) * inv_h + nm.z};
+            float vis = dda_visibility(albedo_occ4, n, q, l);
+            for (int c = 0; c < 3; ++c) d[c] = ((A[c] * color[c]) * ndl) * vis;
+        }
+        float f[3];
+        for (int c = 0; c < 3; ++c) f[c] = (d[c] + A[c] * D[c]) + S[c];
+        if (out_lin4) {
+            out_lin4[4 * i] = f[0]; out_lin4[4 * i + 1] = f[1]; out_lin4[4 * i + 2] = f[2]; out_lin4[4 * i + 3] = 1.0f;
+        }
+        if (out_rgba8) out_rgba8[i] = to8(f[0]) | (to8(f[1]) << 8) | (to8(f[2]) << 16) | (255u << 24);
+    }
+}
+
+/* ------------------------------------------------------------------------- */
 /* A.4  K3 mips                                                               */
 /* ------------------------------------------------------------------------- */
 

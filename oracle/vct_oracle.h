@@ -75,6 +75,16 @@ uint64_t vo_trace(const vo_trace_params* p, const float* r0, const float* pyrami
                   uint32_t w, uint32_t h, uint32_t row_step,
                   float* diffuse4, float* spec4, uint32_t* steps_px, int n_threads);
 
+/* Composite + present (vct_spec.h): per pixel
+ * final = ((albedo*color)*max(n.l,0))*V + albedo*diffuse.rgb + spec.rgb with V
+ * the A.3 shadow walk from the cone origin; out_lin4 (a = 1 / 0 background)
+ * and out_rgba8 (Reinhard, gamma 1/2.2, background = clear colour).  Either
+ * output may be NULL. */
+void vo_composite(uint32_t n, const float g0[3], float extent, const float* albedo_occ4,
+                  const float* pos4, const float* nrm4, const float* alb4, const float* diffuse4,
+                  const float* spec4, uint32_t w, uint32_t h, const float dir_to_light[3],
+                  const float color[3], float* out_lin4, uint32_t* out_rgba8);
+
 /* the spec's log2 (exposed for the known-answer tests) */
 float vo_log2(float x);
 

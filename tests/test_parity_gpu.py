@@ -275,3 +275,37 @@ def test_voxelize_reproducible_and_rerun(gpu_ready):
     a2 = ctx.download_accum()
     assert np.array_equal(a1[0], a2[0]) and np.array_equal(a1[1], a2[1])
     ctx.close()
+
+
+@pytest.mark.parametrize("name,n", [("cornell", 32), ("atrium", 64)])
+def test_composite_matches_oracle(gpu_ready, oracle_mod, name, n):
+    """Row f3: composite + present on the GPU equals the oracle: linear output
+    bit-exact, RGBA8 within 1 (powf differs by an ulp between libm and the device)."""
+    import torch
+    from vct import scenes
+    O = oracle_mod
+    w, h = 96, 64
+    ctx, s, arrs, (g0, E) = gpu_pipeline(n, name)
+    (pos, nrm, alb), cam = _gbuf("scene", s, None, g0, E, w, h)
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    gb = [torch.from_numpy(a).to(dev) for a in (pos, nrm, alb)]
+    d = torch.empty((h, w, 4), device=dev)
+    sp = torch.empty((h, w, 4), device=dev)
+    ctx.trace_device(*gb, w, h, cam.position, d, sp)
+    lin = torch.empty((h, w, 4), device=dev)
+    rgba = torch.empty((h, w), dtype=torch.int32, device=dev)
+    ctx.composite_device(*gb, d, sp, w, h, scenes.LIGHT_DIR, scenes.LIGHT_COLOR, out_linear4=lin, out_rgba8=rgba)
+    torch.cuda.synchronize()
+    ao, _ = ctx.download_voxels()
+    ref_lin, ref_rgba = O.composite(n, g0, E, ao, pos, nrm, alb, d.cpu().numpy(), sp.cpu().numpy(),
+                                    scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    assert np.array_equal(lin.cpu().numpy(), ref_lin)
+    got = rgba.cpu().numpy().view(np.uint32)
+    for sh in (0, 8, 16, 24):
+        a = ((got >> sh) & 255).astype(np.int64)
+        b = ((ref_rgba >> sh) & 255).astype(np.int64)
+        assert np.abs(a - b).max() <= 1
+    assert (pos[..., 3] != 0).any() and (ref_lin[..., :3] > 0).any()
+    # the shadow term matters on these scenes: some lit-facing pixels are shadowed
+    ctx.close()

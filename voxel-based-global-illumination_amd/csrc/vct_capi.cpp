@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <initializer_list>
 #include <new>
 #include <string>
 #include "vct_internal.h"
@@ -347,6 +348,32 @@ vct_status vct_gbuffer_raycast_device(vct_ctx* c, const vct_camera* cam, uint32_
     vct_status st = use_device(c);
     if (st != VCT_OK) return st;
     VCT_HIP(launch_raycast(c, cam, w, h, rough, (float4*)pos4, (float4*)nrm4, (float4*)alb4), "raycast");
+    return VCT_OK;
+}
+
+vct_status vct_composite_device(vct_ctx* c, const float* pos4, const float* nrm4, const float* alb4,
+                                const float* diffuse4, const float* spec4, uint32_t w, uint32_t h,
+                                const float dir_to_light[3], const float color[3], float* out_linear4,
+                                uint32_t* out_rgba8) {
+    if (!c || !pos4 || !nrm4 || !alb4 || !diffuse4 || !spec4 || !dir_to_light || !color || w == 0 || h == 0)
+        return VCT_EINVAL;
+    if (!out_linear4 && !out_rgba8) return fail(c, VCT_EINVAL, "composite: no output");
+    if ((uint64_t)w * h > 0x7fffffffull) return fail(c, VCT_EINVAL, "composite: frame too large");
+    if (!c->grid.voxelized) return fail(c, VCT_ESTATE, "composite before voxelize");
+    for (const void* p : {(const void*)pos4, (const void*)nrm4, (const void*)alb4, (const void*)diffuse4,
+                          (const void*)spec4, (const void*)out_linear4})
+        if (((uintptr_t)p & 15u) != 0) return fail(c, VCT_EINVAL, "composite: float4 buffers must be 16-byte aligned");
+    if (((uintptr_t)out_rgba8 & 3u) != 0) return fail(c, VCT_EINVAL, "composite: rgba8 buffer must be 4-byte aligned");
+    float l[3] = {dir_to_light[0], dir_to_light[1], dir_to_light[2]};   // normalized as vct_inject_directional
+    const float len = sqrtf((l[0] * l[0] + l[1] * l[1]) + l[2] * l[2]);
+    if (!(len > 0.0f) || !std::isfinite(len)) return fail(c, VCT_EINVAL, "zero or non-finite light direction");
+    l[0] = l[0] / len; l[1] = l[1] / len; l[2] = l[2] / len;
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(launch_composite(c, (const float4*)pos4, (const float4*)nrm4, (const float4*)alb4,
+                             (const float4*)diffuse4, (const float4*)spec4, w, h, l, color, (float4*)out_linear4,
+                             out_rgba8),
+            "composite");
     return VCT_OK;
 }
 

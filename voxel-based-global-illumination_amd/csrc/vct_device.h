@@ -41,6 +41,39 @@ __host__ __device__ __forceinline__ float spec_log2(float x) {
     return fmaf(ln, VCT_INV_LN2, (float)e);
 }
 
+__device__ __forceinline__ bool occ_at(const unsigned long long* __restrict__ bits, int n, int x, int y, int z) {
+    size_t v = (size_t)x + (size_t)n * ((size_t)y + (size_t)n * (size_t)z);
+    return (bits[v >> 6] >> (v & 63)) & 1ull;
+}
+
+// A.3 shadow walk (Amanatides-Woo) from q (voxel units) toward l over the
+// level-0 occupancy bits: 1 = leaves the grid unblocked, 0 = hits a voxel.
+__device__ __forceinline__ float dda_visibility(const unsigned long long* __restrict__ bits, int N, float qx, float qy,
+                                float qz, float lx, float ly, float lz) {
+    int vx = (int)floorf(qx), vy = (int)floorf(qy), vz = (int)floorf(qz);
+    if (vx < 0 || vy < 0 || vz < 0 || vx >= N || vy >= N || vz >= N) return 1.0f;
+    int sx = lx > 0.0f ? 1 : (lx < 0.0f ? -1 : 0);
+    int sy = ly > 0.0f ? 1 : (ly < 0.0f ? -1 : 0);
+    int sz = lz > 0.0f ? 1 : (lz < 0.0f ? -1 : 0);
+    const float inf = __builtin_inff();
+    float tdx = sx ? 1.0f / fabsf(lx) : inf;
+    float tdy = sy ? 1.0f / fabsf(ly) : inf;
+    float tdz = sz ? 1.0f / fabsf(lz) : inf;
+    float tmx = sx > 0 ? ((float)(vx + 1) - qx) * tdx : (sx < 0 ? (qx - (float)vx) * tdx : inf);
+    float tmy = sy > 0 ? ((float)(vy + 1) - qy) * tdy : (sy < 0 ? (qy - (float)vy) * tdy : inf);
+    float tmz = sz > 0 ? ((float)(vz + 1) - qz) * tdz : (sz < 0 ? (qz - (float)vz) * tdz : inf);
+    for (;;) {
+        if (occ_at(bits, N, vx, vy, vz)) return 0.0f;
+        if (tmx <= tmy && tmx <= tmz) {
+            vx += sx; if (vx < 0 || vx >= N) return 1.0f; tmx = tmx + tdx;
+        } else if (tmy <= tmz) {
+            vy += sy; if (vy < 0 || vy >= N) return 1.0f; tmy = tmy + tdy;
+        } else {
+            vz += sz; if (vz < 0 || vz >= N) return 1.0f; tmz = tmz + tdz;
+        }
+    }
+}
+
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
     return (ax * bx + ay * by) + az * bz;
 }

@@ -94,6 +94,50 @@ __global__ void __launch_bounds__(256) k_raycast(RayK k) {
     k.alb[p] = make_float4(kd.x, kd.y, kd.z, k.rough);
 }
 
+// ---- composite + present (spec in vct_spec.h) ------------
+struct CompK {
+    const float4 *pos, *nrm, *alb, *diff, *spec;
+    const unsigned long long* bits;
+    int n, w, h;
+    float g0x, g0y, g0z, inv_h;
+    float lx, ly, lz, cr, cg, cb;
+    float4* lin;
+    uint32_t* rgba8;
+};
+
+__device__ __forceinline__ uint32_t to8(float v) {   // Reinhard, gamma 1/2.2, round half away
+    v = v / (1.0f + v);
+    v = powf(v < 0.0f ? 0.0f : v, VCT_INV_GAMMA);
+    const int q = (int)lroundf(v * 255.0f);
+    return (uint32_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
+}
+
+__global__ void __launch_bounds__(256) k_composite(CompK k) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= (uint32_t)k.w * (uint32_t)k.h) return;
+    const float4 P = k.pos[i];
+    if (P.w == 0.0f) {   // background: the reference's clear colour
+        if (k.lin) k.lin[i] = make_float4(VCT_CLEAR_R, VCT_CLEAR_G, VCT_CLEAR_B, 0.0f);
+        if (k.rgba8)
+            k.rgba8[i] = (uint32_t)lroundf(VCT_CLEAR_R * 255.0f) | ((uint32_t)lroundf(VCT_CLEAR_G * 255.0f) << 8) |
+                         ((uint32_t)lroundf(VCT_CLEAR_B * 255.0f) << 16) | (255u << 24);
+        return;
+    }
+    const float4 N = k.nrm[i], A = k.alb[i], D = k.diff[i], S = k.spec[i];
+    const float ndl = dot3(N.x, N.y, N.z, k.lx, k.ly, k.lz);
+    float dr = 0.0f, dg = 0.0f, db = 0.0f;
+    if (ndl > 0.0f) {
+        const float vis = dda_visibility(k.bits, k.n, (P.x - k.g0x) * k.inv_h + N.x, (P.y - k.g0y) * k.inv_h + N.y,
+                                         (P.z - k.g0z) * k.inv_h + N.z, k.lx, k.ly, k.lz);
+        dr = ((A.x * k.cr) * ndl) * vis;
+        dg = ((A.y * k.cg) * ndl) * vis;
+        db = ((A.z * k.cb) * ndl) * vis;
+    }
+    const float fr = (dr + A.x * D.x) + S.x, fg = (dg + A.y * D.y) + S.y, fb = (db + A.z * D.z) + S.z;
+    if (k.lin) k.lin[i] = make_float4(fr, fg, fb, 1.0f);
+    if (k.rgba8) k.rgba8[i] = to8(fr) | (to8(fg) << 8) | (to8(fb) << 16) | (255u << 24);
+}
+
 }  // namespace
 
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
@@ -131,6 +175,23 @@ hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_
     k.pos = pos; k.nrm = nrm; k.alb = alb;
     dim3 grid((w + 15) / 16, (h + 15) / 16);
     hipLaunchKernelGGL(k_raycast, grid, dim3(256), 0, c->stream, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_composite(vct_ctx* c, const float4* pos, const float4* nrm, const float4* alb,
+                            const float4* diff, const float4* spec, uint32_t w, uint32_t h, const float l[3],
+                            const float color[3], float4* lin, uint32_t* rgba8) {
+    const Grid& g = c->grid;
+    CompK k;
+    k.pos = pos; k.nrm = nrm; k.alb = alb; k.diff = diff; k.spec = spec;
+    k.bits = g.occ_bits;
+    k.n = (int)g.n; k.w = (int)w; k.h = (int)h;
+    k.g0x = g.g0[0]; k.g0y = g.g0[1]; k.g0z = g.g0[2]; k.inv_h = g.inv_h;
+    k.lx = l[0]; k.ly = l[1]; k.lz = l[2];
+    k.cr = color[0]; k.cg = color[1]; k.cb = color[2];
+    k.lin = lin; k.rgba8 = rgba8;
+    const uint32_t px = w * h;
+    hipLaunchKernelGGL(k_composite, dim3((px + 255) / 256), dim3(256), 0, c->stream, k);
     return hipGetLastError();
 }
 

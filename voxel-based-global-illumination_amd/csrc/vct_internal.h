@@ -67,6 +67,10 @@ hipError_t launch_mips(vct_ctx* c);
 hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a);
 hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t w, uint32_t h, uint32_t world,
                          float4* frame);
+// composite + present (row f3)
+hipError_t launch_composite(vct_ctx* c, const float4* pos, const float4* nrm, const float4* alb,
+                            const float4* diff, const float4* spec, uint32_t w, uint32_t h, const float l[3],
+                            const float color[3], float4* lin, uint32_t* rgba8);
 // G-buffer
 hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
                           float4* pos, float4* nrm, float4* alb);

@@ -289,37 +289,6 @@ __global__ void __launch_bounds__(256) k1_resolve(const long long* __restrict__ 
 }
 
 // ---- K2 injection ----------------------------------------------------------
-__device__ __forceinline__ bool occ_at(const unsigned long long* __restrict__ bits, int n, int x, int y, int z) {
-    size_t v = (size_t)x + (size_t)n * ((size_t)y + (size_t)n * (size_t)z);
-    return (bits[v >> 6] >> (v & 63)) & 1ull;
-}
-
-__device__ float dda_visibility(const unsigned long long* __restrict__ bits, int N, float qx, float qy,
-                                float qz, float lx, float ly, float lz) {
-    int vx = (int)floorf(qx), vy = (int)floorf(qy), vz = (int)floorf(qz);
-    if (vx < 0 || vy < 0 || vz < 0 || vx >= N || vy >= N || vz >= N) return 1.0f;
-    int sx = lx > 0.0f ? 1 : (lx < 0.0f ? -1 : 0);
-    int sy = ly > 0.0f ? 1 : (ly < 0.0f ? -1 : 0);
-    int sz = lz > 0.0f ? 1 : (lz < 0.0f ? -1 : 0);
-    const float inf = __builtin_inff();
-    float tdx = sx ? 1.0f / fabsf(lx) : inf;
-    float tdy = sy ? 1.0f / fabsf(ly) : inf;
-    float tdz = sz ? 1.0f / fabsf(lz) : inf;
-    float tmx = sx > 0 ? ((float)(vx + 1) - qx) * tdx : (sx < 0 ? (qx - (float)vx) * tdx : inf);
-    float tmy = sy > 0 ? ((float)(vy + 1) - qy) * tdy : (sy < 0 ? (qy - (float)vy) * tdy : inf);
-    float tmz = sz > 0 ? ((float)(vz + 1) - qz) * tdz : (sz < 0 ? (qz - (float)vz) * tdz : inf);
-    for (;;) {
-        if (occ_at(bits, N, vx, vy, vz)) return 0.0f;
-        if (tmx <= tmy && tmx <= tmz) {
-            vx += sx; if (vx < 0 || vx >= N) return 1.0f; tmx = tmx + tdx;
-        } else if (tmy <= tmz) {
-            vy += sy; if (vy < 0 || vy >= N) return 1.0f; tmy = tmy + tdy;
-        } else {
-            vz += sz; if (vz < 0 || vz >= N) return 1.0f; tmz = tmz + tdz;
-        }
-    }
-}
-
 __global__ void __launch_bounds__(256) k2_inject(const float4* __restrict__ albedo_occ,
                                                  const float4* __restrict__ normal,
                                                  const unsigned long long* __restrict__ bits, int n,

@@ -90,27 +90,29 @@ void ConeTraceRenderer::Render() {
 }
 
 bool ConeTraceRenderer::WritePPM(const std::string& path) {
+    // row f3: composite + present on the device (include/vct.h vct_composite_device), then dump
     if (!ctx_) return false;
     const size_t px = (size_t)s_.width * s_.height;
-    std::vector<float> d(px * 4), sp(px * 4), alb(px * 4), pos(px * 4);
-    if (!check(vct_memcpy(ctx_, d.data(), out_[0], px * 16, 1), "download") ||
-        !check(vct_memcpy(ctx_, sp.data(), out_[1], px * 16, 1), "download") ||
-        !check(vct_memcpy(ctx_, alb.data(), gb_[2], px * 16, 1), "download") ||
-        !check(vct_memcpy(ctx_, pos.data(), gb_[0], px * 16, 1), "download"))
-        return false;
+    void* rgba = nullptr;
+    if (!check(vct_device_alloc(ctx_, px * 4, &rgba), "alloc rgba8")) return false;
+    std::vector<uint32_t> img(px);
+    const bool ok = check(vct_composite_device(ctx_, (const float*)gb_[0], (const float*)gb_[1], (const float*)gb_[2],
+                                               (const float*)out_[0], (const float*)out_[1], s_.width, s_.height,
+                                               s_.light_dir, s_.light_color, nullptr, (uint32_t*)rgba),
+                          "vct_composite_device") &&
+                    check(vct_memcpy(ctx_, img.data(), rgba, px * 4, 1), "download rgba8");
+    vct_device_free(ctx_, rgba);
+    if (!ok) return false;
     FILE* f = std::fopen(path.c_str(), "wb");
     if (!f) return false;
     std::fprintf(f, "P6\n%u %u\n255\n", s_.width, s_.height);
     std::vector<unsigned char> row(s_.width * 3);
     for (uint32_t y = 0; y < s_.height; ++y) {
-        for (uint32_t x = 0; x < s_.width; ++x) {
-            const size_t i = (size_t)y * s_.width + x;
-            for (int c = 0; c < 3; ++c) {
-                float v = pos[4 * i + 3] != 0.0f ? alb[4 * i + c] * d[4 * i + c] * 4.0f + sp[4 * i + c] : 0.2f;
-                v = v / (1.0f + v);                      // Reinhard
-                v = std::pow(v < 0 ? 0 : v, 1.0f / 2.2f);
-                row[3 * x + c] = (unsigned char)std::lround(v * 255.0f);
-            }
+        for (uint32_t x = 0; x < s_.width; ++x) {               // row 0 = top (the G-buffer's ray rule)
+            const uint32_t c = img[(size_t)y * s_.width + x];
+            row[3 * x] = (unsigned char)(c & 255);
+            row[3 * x + 1] = (unsigned char)((c >> 8) & 255);
+            row[3 * x + 2] = (unsigned char)((c >> 16) & 255);
         }
         std::fwrite(row.data(), 1, row.size(), f);
     }

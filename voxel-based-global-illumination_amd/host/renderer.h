@@ -46,7 +46,7 @@ public:
     const std::string& error() const { return error_; }
     double last_trace_ms() const { return last_ms_; }
     unsigned long long last_cone_steps() const { return last_steps_; }
-    // composite (albedo * indirect irradiance + specular) -> binary PPM
+    // composite + present (vct_composite_device: direct + albedo * indirect + specular) -> binary PPM
     bool WritePPM(const std::string& path);
 
 private:

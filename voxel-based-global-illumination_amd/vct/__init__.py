@@ -181,6 +181,16 @@ class Context:
         self._check(self.lib.vct_gbuffer_raycast_device(self.h, C.byref(c), width, height, float(roughness),
                                                         ptr(pos4), ptr(nrm4), ptr(alb4)), "raycast")
 
+    def composite_device(self, pos4, nrm4, alb4, diffuse4, spec4, width, height, dir_to_light,
+                         color=(1.0, 1.0, 1.0), out_linear4=None, out_rgba8=None):
+        """Row f3 composite + present on device buffers (torch tensors or raw pointers)."""
+        ptr = lambda t: None if t is None else (t if isinstance(t, int) else t.data_ptr())
+        l = (C.c_float * 3)(*[float(x) for x in dir_to_light])
+        c = (C.c_float * 3)(*[float(x) for x in color])
+        self._check(self.lib.vct_composite_device(self.h, ptr(pos4), ptr(nrm4), ptr(alb4), ptr(diffuse4),
+                                                  ptr(spec4), width, height, l, c, ptr(out_linear4),
+                                                  ptr(out_rgba8)), "composite")
+
     # -- grid access ------------------------------------------------------
     def download_level(self, level: int, face: int = 0) -> np.ndarray:
         nl, _ = self.level_dims(level)
