@@ -143,6 +143,15 @@ vct_status vct_gbuffer_raycast_device(vct_ctx* ctx, const vct_camera* cam, uint3
                                       uint32_t height, float roughness, float* pos4,
                                       float* nrm4, float* alb4);
 
+/* Same G-buffer as vct_gbuffer_raycast_device, for mesh scenes (SURVEY 8f row
+ * f2): the triangles are binned into 16x16-pixel screen tiles through the
+ * reference camera (perspective(Zoom, w/h, near, far) + lookAt, r_voxelization.cpp:
+ * 16-23), and each pixel's ray is intersected only with its tile's triangles.
+ * Ties go to the lower triangle index, so the output equals the brute-force
+ * caster's bit for bit.  One small device->host read per call sizes the bins. */
+vct_status vct_gbuffer_raster_device(vct_ctx* ctx, const vct_camera* cam, uint32_t width, uint32_t height,
+                                     float roughness, float* pos4, float* nrm4, float* alb4);
+
 /* ---- composite + present -------------------------------
  * final = direct + albedo * diffuse.rgb + spec.rgb per pixel, direct = albedo *
  * color * max(n.l, 0) * shadow (the K2 voxel walk from the cone origin), into

@@ -351,6 +351,18 @@ vct_status vct_gbuffer_raycast_device(vct_ctx* c, const vct_camera* cam, uint32_
     return VCT_OK;
 }
 
+vct_status vct_gbuffer_raster_device(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
+                                     float* pos4, float* nrm4, float* alb4) {
+    if (!c || !cam || !pos4 || !nrm4 || !alb4 || w == 0 || h == 0) return VCT_EINVAL;
+    if ((uint64_t)w * h > 0x7fffffffull || (uint64_t)((w + 15) / 16) * ((h + 15) / 16) > (1u << 20))
+        return fail(c, VCT_EINVAL, "raster: frame too large");
+    if (!c->mesh.tri) return fail(c, VCT_ESTATE, "raster before voxelize");
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(launch_gbuffer_binned(c, cam, w, h, rough, (float4*)pos4, (float4*)nrm4, (float4*)alb4), "raster");
+    return VCT_OK;
+}
+
 vct_status vct_composite_device(vct_ctx* c, const float* pos4, const float* nrm4, const float* alb4,
                                 const float* diffuse4, const float* spec4, uint32_t w, uint32_t h,
                                 const float dir_to_light[3], const float color[3], float* out_linear4,

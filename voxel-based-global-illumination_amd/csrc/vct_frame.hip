@@ -38,44 +38,36 @@ struct RayK {
 
 constexpr int kRayChunk = 256;
 
-__global__ void __launch_bounds__(256) k_raycast(RayK k) {
-    __shared__ float4 sh[kRayChunk * 4];
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+// Moller-Trumbore: ray parameter t of the hit, or -1 (no hit / parallel)
+__device__ __forceinline__ float ray_tri(float4 v0, float4 e1, float4 e2, float px, float py, float pz, float dx,
+                                         float dy, float dz) {
+    const float pvx = dy * e2.z - dz * e2.y, pvy = dz * e2.x - dx * e2.z, pvz = dx * e2.y - dy * e2.x;
+    const float det = dot3(e1.x, e1.y, e1.z, pvx, pvy, pvz);
+    if (fabsf(det) < 1e-12f) return -1.0f;
+    const float inv = 1.0f / det;
+    const float tx = px - v0.x, ty = py - v0.y, tz = pz - v0.z;
+    const float u = dot3(tx, ty, tz, pvx, pvy, pvz) * inv;
+    if (u < 0.0f || u > 1.0f) return -1.0f;
+    const float qx = ty * e1.z - tz * e1.y, qy = tz * e1.x - tx * e1.z, qz = tx * e1.y - ty * e1.x;
+    const float v = dot3(dx, dy, dz, qx, qy, qz) * inv;
+    if (v < 0.0f || u + v > 1.0f) return -1.0f;
+    return dot3(e2.x, e2.y, e2.z, qx, qy, qz) * inv;
+}
+
+// pixel (x, y) -> unit ray direction (row 0 = top; reference camera, r_voxelization.cpp:16-23)
+__device__ __forceinline__ void pixel_ray(const RayK& k, int x, int y, float& dx, float& dy, float& dz) {
     const float ndx = (2.0f * ((float)x + 0.5f) / (float)k.w - 1.0f) * k.tan_half * k.aspect;
     const float ndy = (1.0f - 2.0f * ((float)y + 0.5f) / (float)k.h) * k.tan_half;
-    float dx = k.fx + ndx * k.rx + ndy * k.ux;
-    float dy = k.fy + ndx * k.ry + ndy * k.uy;
-    float dz = k.fz + ndx * k.rz + ndy * k.uz;
+    dx = k.fx + ndx * k.rx + ndy * k.ux;
+    dy = k.fy + ndx * k.ry + ndy * k.uy;
+    dz = k.fz + ndx * k.rz + ndy * k.uz;
     const float il = 1.0f / sqrtf(dot3(dx, dy, dz, dx, dy, dz));
     dx *= il; dy *= il; dz *= il;
-    float best = __builtin_inff();
-    int hit = -1;
-    for (uint32_t base = 0; base < k.n_tri; base += kRayChunk) {
-        __syncthreads();
-        for (int i = threadIdx.x; i < kRayChunk * 4; i += 256) {
-            uint32_t tri = base + i / 4;
-            sh[i] = tri < k.n_tri ? k.tri[(size_t)tri * 4 + (i & 3)] : make_float4(0, 0, 0, 0);
-        }
-        __syncthreads();
-        const uint32_t cnt = min((uint32_t)kRayChunk, k.n_tri - base);
-        for (uint32_t j = 0; j < cnt; ++j) {
-            const float4 v0 = sh[4 * j], e1 = sh[4 * j + 1], e2 = sh[4 * j + 2];
-            const float pvx = dy * e2.z - dz * e2.y, pvy = dz * e2.x - dx * e2.z, pvz = dx * e2.y - dy * e2.x;
-            const float det = dot3(e1.x, e1.y, e1.z, pvx, pvy, pvz);
-            if (fabsf(det) < 1e-12f) continue;
-            const float inv = 1.0f / det;
-            const float tx = k.px - v0.x, ty = k.py - v0.y, tz = k.pz - v0.z;
-            const float u = dot3(tx, ty, tz, pvx, pvy, pvz) * inv;
-            if (u < 0.0f || u > 1.0f) continue;
-            const float qx = ty * e1.z - tz * e1.y, qy = tz * e1.x - tx * e1.z, qz = tx * e1.y - ty * e1.x;
-            const float v = dot3(dx, dy, dz, qx, qy, qz) * inv;
-            if (v < 0.0f || u + v > 1.0f) continue;
-            const float t = dot3(e2.x, e2.y, e2.z, qx, qy, qz) * inv;
-            if (t > 0.0f && t < best) { best = t; hit = (int)(base + j); }
-        }
-    }
-    if (x >= k.w || y >= k.h) return;
+}
+
+// G-buffer texel of the nearest hit (shared by the brute-force and the binned pass)
+__device__ __forceinline__ void write_gbuffer(const RayK& k, int x, int y, float dx, float dy, float dz, float best,
+                                              int hit) {
     const size_t p = (size_t)y * k.w + x;
     const float depth = best * dot3(dx, dy, dz, k.fx, k.fy, k.fz);
     if (hit < 0 || depth < k.near_p || depth > k.far_p) {
@@ -92,6 +84,166 @@ __global__ void __launch_bounds__(256) k_raycast(RayK k) {
     k.pos[p] = make_float4(k.px + dx * best, k.py + dy * best, k.pz + dz * best, 1.0f);
     k.nrm[p] = make_float4(nx, ny, nz, 0.0f);
     k.alb[p] = make_float4(kd.x, kd.y, kd.z, k.rough);
+}
+
+__global__ void __launch_bounds__(256) k_raycast(RayK k) {
+    __shared__ float4 sh[kRayChunk * 4];
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    float dx, dy, dz;
+    pixel_ray(k, x, y, dx, dy, dz);
+    float best = __builtin_inff();
+    int hit = -1;
+    for (uint32_t base = 0; base < k.n_tri; base += kRayChunk) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < kRayChunk * 4; i += 256) {
+            uint32_t tri = base + i / 4;
+            sh[i] = tri < k.n_tri ? k.tri[(size_t)tri * 4 + (i & 3)] : make_float4(0, 0, 0, 0);
+        }
+        __syncthreads();
+        const uint32_t cnt = min((uint32_t)kRayChunk, k.n_tri - base);
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const float t = ray_tri(sh[4 * j], sh[4 * j + 1], sh[4 * j + 2], k.px, k.py, k.pz, dx, dy, dz);
+            if (t > 0.0f && t < best) { best = t; hit = (int)(base + j); }
+        }
+    }
+    if (x >= k.w || y >= k.h) return;
+    write_gbuffer(k, x, y, dx, dy, dz, best, hit);
+}
+
+// ---- tile-binned G-buffer pass ------------------------
+// Screen-space binning of the triangles into 16x16-pixel tiles (projected
+// through the reference camera; clipped to cz >= 1e-5 so the bounding boxes are
+// conservative), then one workgroup per tile intersects its pixels' rays with
+// the tile's triangles only.  Ties in t go to the lower triangle index, so the
+// result equals the brute-force caster's bit for bit, at O(px x tris per tile).
+constexpr int kGT = 16;
+
+struct BinK {
+    RayK r;
+    int tiles_x, tiles_y;
+    float sxs, sys;                // pixel scale: X = w/2 + (cx/cz) sxs, Y = h/2 - (cy/cz) sys
+    int4* rect;                    // per triangle tile rectangle (x0 > x1: culled)
+    uint32_t* count;               // per tile: triangles, then the fill cursor
+    uint32_t* offset;              // per tile: exclusive prefix of count; [n_tiles] = total
+    uint32_t* bins;                // triangle indices grouped by tile
+};
+
+__global__ void __launch_bounds__(256) k_bin_rect(BinK k) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= k.r.n_tri) return;
+    const RayK& r = k.r;
+    const float4 v0 = r.tri[(size_t)t * 4], e1 = r.tri[(size_t)t * 4 + 1], e2 = r.tri[(size_t)t * 4 + 2];
+    float c[3][3];
+    const float vx[3] = {v0.x, v0.x + e1.x, v0.x + e2.x}, vy[3] = {v0.y, v0.y + e1.y, v0.y + e2.y},
+                vz[3] = {v0.z, v0.z + e1.z, v0.z + e2.z};
+    for (int i = 0; i < 3; ++i) {
+        const float qx = vx[i] - r.px, qy = vy[i] - r.py, qz = vz[i] - r.pz;
+        c[i][0] = dot3(qx, qy, qz, r.rx, r.ry, r.rz);
+        c[i][1] = dot3(qx, qy, qz, r.ux, r.uy, r.uz);
+        c[i][2] = dot3(qx, qy, qz, r.fx, r.fy, r.fz);
+    }
+    // clip the triangle to cz >= zc (Sutherland-Hodgman, one plane), project the polygon
+    const float zc = 1e-5f;
+    float lo_x = __builtin_inff(), lo_y = __builtin_inff(), hi_x = -__builtin_inff(), hi_y = -__builtin_inff();
+    bool any = false, beyond = true;
+    for (int i = 0; i < 3; ++i) {
+        const float* a = c[i];
+        const float* b = c[(i + 1) % 3];
+        beyond &= a[2] > r.far_p;
+        const bool ina = a[2] >= zc, inb = b[2] >= zc;
+        float p[2][3];
+        int np = 0;
+        if (ina) { p[np][0] = a[0]; p[np][1] = a[1]; p[np][2] = a[2]; ++np; }
+        if (ina != inb) {
+            const float s = (zc - a[2]) / (b[2] - a[2]);
+            p[np][0] = a[0] + (b[0] - a[0]) * s; p[np][1] = a[1] + (b[1] - a[1]) * s; p[np][2] = zc; ++np;
+        }
+        for (int j = 0; j < np; ++j) {
+            const float X = 0.5f * (float)r.w + (p[j][0] / p[j][2]) * k.sxs;
+            const float Y = 0.5f * (float)r.h - (p[j][1] / p[j][2]) * k.sys;
+            lo_x = fminf(lo_x, X); hi_x = fmaxf(hi_x, X); lo_y = fminf(lo_y, Y); hi_y = fmaxf(hi_y, Y);
+            any = true;
+        }
+    }
+    int4 rc = make_int4(1, 0, 0, 0);   // culled
+    if (any && !beyond) {
+        // one pixel of margin, pixel centres at +0.5
+        const float x0 = fmaxf(lo_x - 1.5f, 0.0f), x1 = fminf(hi_x + 0.5f, (float)(r.w - 1));
+        const float y0 = fmaxf(lo_y - 1.5f, 0.0f), y1 = fminf(hi_y + 0.5f, (float)(r.h - 1));
+        if (x0 <= x1 && y0 <= y1)
+            rc = make_int4((int)x0 / kGT, (int)y0 / kGT, (int)x1 / kGT, (int)y1 / kGT);
+    }
+    k.rect[t] = rc;
+    for (int ty = rc.y; ty <= rc.w && rc.x <= rc.z; ++ty)
+        for (int tx = rc.x; tx <= rc.z; ++tx) atomicAdd(&k.count[ty * k.tiles_x + tx], 1u);
+}
+
+// exclusive scan of the tile counts (one workgroup; n_tiles <= 64K at 4K), count -> 0 (fill cursor)
+__global__ void __launch_bounds__(1024) k_bin_scan(uint32_t* count, uint32_t* offset, uint32_t n) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (n + 1023) / 1024, lo = threadIdx.x * per, hi = min(lo + per, n);
+    uint32_t s = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += count[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - s;
+    for (uint32_t i = lo; i < hi; ++i) {
+        offset[i] = run;
+        run += count[i];
+        count[i] = 0u;
+    }
+    if (threadIdx.x == 1023) offset[n] = part[1023];
+}
+
+__global__ void __launch_bounds__(256) k_bin_fill(BinK k) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= k.r.n_tri) return;
+    const int4 rc = k.rect[t];
+    for (int ty = rc.y; ty <= rc.w && rc.x <= rc.z; ++ty)
+        for (int tx = rc.x; tx <= rc.z; ++tx) {
+            const int tile = ty * k.tiles_x + tx;
+            k.bins[k.offset[tile] + atomicAdd(&k.count[tile], 1u)] = t;
+        }
+}
+
+__global__ void __launch_bounds__(256) k_bin_raster(BinK k) {
+    __shared__ float4 sh[kRayChunk * 3];
+    __shared__ uint32_t sid[kRayChunk];
+    const RayK& r = k.r;
+    const int tile = (int)blockIdx.x;
+    const int x = (tile % k.tiles_x) * kGT + (int)(threadIdx.x & 15);
+    const int y = (tile / k.tiles_x) * kGT + (int)(threadIdx.x >> 4);
+    float dx, dy, dz;
+    pixel_ray(r, x, y, dx, dy, dz);
+    float best = __builtin_inff();
+    int hit = -1;
+    const uint32_t beg = k.offset[tile], end = k.offset[tile + 1];
+    for (uint32_t base = beg; base < end; base += kRayChunk) {
+        __syncthreads();
+        const uint32_t cnt = min((uint32_t)kRayChunk, end - base);
+        if (threadIdx.x < cnt) {
+            const uint32_t t = k.bins[base + threadIdx.x];
+            sid[threadIdx.x] = t;
+            sh[3 * threadIdx.x] = r.tri[(size_t)t * 4];
+            sh[3 * threadIdx.x + 1] = r.tri[(size_t)t * 4 + 1];
+            sh[3 * threadIdx.x + 2] = r.tri[(size_t)t * 4 + 2];
+        }
+        __syncthreads();
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const float t = ray_tri(sh[3 * j], sh[3 * j + 1], sh[3 * j + 2], r.px, r.py, r.pz, dx, dy, dz);
+            const int id = (int)sid[j];
+            if (t > 0.0f && (t < best || (t == best && id < hit))) { best = t; hit = id; }
+        }
+    }
+    if (x >= r.w || y >= r.h) return;
+    write_gbuffer(r, x, y, dx, dy, dz, best, hit);
 }
 
 // ---- composite + present (spec in vct_spec.h) ------------
@@ -159,8 +311,8 @@ hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t w, uint32_
     return hipGetLastError();
 }
 
-hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
-                          float4* pos, float4* nrm, float4* alb) {
+static RayK ray_params(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough, float4* pos,
+                       float4* nrm, float4* alb) {
     RayK k;
     k.tri = c->mesh.tri; k.n_tri = c->mesh.n_tri;
     k.w = (int)w; k.h = (int)h;
@@ -173,8 +325,45 @@ hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_
     k.near_p = cam->near_plane; k.far_p = cam->far_plane;
     k.rough = rough;
     k.pos = pos; k.nrm = nrm; k.alb = alb;
+    return k;
+}
+
+hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
+                          float4* pos, float4* nrm, float4* alb) {
+    const RayK k = ray_params(c, cam, w, h, rough, pos, nrm, alb);
     dim3 grid((w + 15) / 16, (h + 15) / 16);
     hipLaunchKernelGGL(k_raycast, grid, dim3(256), 0, c->stream, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_gbuffer_binned(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
+                                 float4* pos, float4* nrm, float4* alb) {
+    BinK k;
+    k.r = ray_params(c, cam, w, h, rough, pos, nrm, alb);
+    k.tiles_x = (int)((w + kGT - 1) / kGT);
+    k.tiles_y = (int)((h + kGT - 1) / kGT);
+    k.sxs = 0.5f * (float)w / (k.r.tan_half * k.r.aspect);
+    k.sys = 0.5f * (float)h / k.r.tan_half;
+    const uint32_t n_tiles = (uint32_t)(k.tiles_x * k.tiles_y), n_tri = c->mesh.n_tri;
+    const size_t b_rect = ((size_t)n_tri * sizeof(int4) + 255) & ~(size_t)255;
+    const size_t b_cnt = ((size_t)n_tiles * 4 + 255) & ~(size_t)255;
+    void* sp;
+    hipError_t e;
+    if ((e = scratch_get(c, 2, b_rect + b_cnt + (size_t)(n_tiles + 1) * 4, &sp)) != hipSuccess) return e;
+    k.rect = (int4*)sp;
+    k.count = (uint32_t*)((char*)sp + b_rect);
+    k.offset = (uint32_t*)((char*)sp + b_rect + b_cnt);
+    if ((e = hipMemsetAsync(k.count, 0, (size_t)n_tiles * 4, c->stream)) != hipSuccess) return e;
+    const uint32_t tb = (n_tri + 255) / 256;
+    if (n_tri) hipLaunchKernelGGL(k_bin_rect, dim3(tb), dim3(256), 0, c->stream, k);
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, c->stream, k.count, k.offset, n_tiles);
+    uint32_t total = 0;   // bin storage is sized on the host (one small read back per frame)
+    if ((e = hipMemcpyAsync(&total, k.offset + n_tiles, 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return e;
+    if ((e = scratch_get(c, 3, (size_t)(total ? total : 1) * 4, &sp)) != hipSuccess) return e;
+    k.bins = (uint32_t*)sp;
+    if (n_tri && total) hipLaunchKernelGGL(k_bin_fill, dim3(tb), dim3(256), 0, c->stream, k);
+    hipLaunchKernelGGL(k_bin_raster, dim3(n_tiles), dim3(256), 0, c->stream, k);
     return hipGetLastError();
 }
 

@@ -72,6 +72,8 @@ hipError_t launch_composite(vct_ctx* c, const float4* pos, const float4* nrm, co
                             const float4* diff, const float4* spec, uint32_t w, uint32_t h, const float l[3],
                             const float color[3], float4* lin, uint32_t* rgba8);
 // G-buffer
+hipError_t launch_gbuffer_binned(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
+                                 float4* pos, float4* nrm, float4* alb);
 hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
                           float4* pos, float4* nrm, float4* alb);
 

@@ -67,8 +67,8 @@ void ConeTraceRenderer::Render() {
     auto cam = AssetsManager::Instance().ActiveCamera();
     if (!cam) return;
     const vct_camera vc = cam->ToVct();
-    if (!check(vct_gbuffer_raycast_device(ctx_, &vc, s_.width, s_.height, s_.roughness, (float*)gb_[0],
-                                          (float*)gb_[1], (float*)gb_[2]), "raycast"))
+    if (!check(vct_gbuffer_raster_device(ctx_, &vc, s_.width, s_.height, s_.roughness, (float*)gb_[0],
+                                         (float*)gb_[1], (float*)gb_[2]), "G-buffer"))
         return;
     unsigned long long zero = 0;
     if (!check(vct_memcpy(ctx_, counter_, &zero, 8, 0), "reset counter")) return;

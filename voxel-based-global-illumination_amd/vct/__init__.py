@@ -181,6 +181,13 @@ class Context:
         self._check(self.lib.vct_gbuffer_raycast_device(self.h, C.byref(c), width, height, float(roughness),
                                                         ptr(pos4), ptr(nrm4), ptr(alb4)), "raycast")
 
+    def gbuffer_raster_device(self, cam, width, height, roughness, pos4, nrm4, alb4):
+        """Row f2: tile-binned G-buffer pass (same output as gbuffer_raycast_device)."""
+        c = cam.to_ctypes() if hasattr(cam, "to_ctypes") else cam
+        ptr = lambda t: t if isinstance(t, int) else t.data_ptr()
+        self._check(self.lib.vct_gbuffer_raster_device(self.h, C.byref(c), width, height, float(roughness),
+                                                       ptr(pos4), ptr(nrm4), ptr(alb4)), "raster")
+
     def composite_device(self, pos4, nrm4, alb4, diffuse4, spec4, width, height, dir_to_light,
                          color=(1.0, 1.0, 1.0), out_linear4=None, out_rgba8=None):
         """Row f3 composite + present on device buffers (torch tensors or raw pointers)."""
