@@ -283,6 +283,37 @@ def random_obj(seed=11, nverts=60, nfaces=220):
 CASES = {"cube": CUBE, "poly": POLY, "edge": EDGE, "degen": DEGEN, "sphere": sphere_obj(),
          "random": random_obj()}
 
+# The reference's own material library (assets/model/test/nanosuit.mtl, Blender
+# export: Ns/Ni/d/illum/map_* lines) is data: it is stored in the fixture as the
+# MTL input of one case, with a procedural mesh that uses its materials by name.
+REF_MTL = "/root/reference/assets/model/test/nanosuit.mtl"
+NANO_OBJ = """mtllib scene.mtl
+o Visor
+v 0 0 0
+v 1 0 0
+v 1 1 0
+v 0 1 0
+v 0.5 0.5 1
+vt 0 0
+vt 1 0
+vt 1 1
+vt 0 1
+vn 0 0 -1
+vn 0 0.7071 0.7071
+usemtl Glass
+f 1/1/1 2/2/1 3/3/1 4/4/1
+usemtl Helmet
+f 1/1/2 2/2/2 5/3/2
+f 2/2/2 3/3/2 5/4/2
+o Body
+usemtl Body
+f 3/1/2 4/2/2 5/3/2
+usemtl Arm
+f 4/1/2 1/2/2 5/3/2
+usemtl Leg
+f 1/1/1 3/3/1 2/2/1
+"""
+
 
 def import_with_assimp(lib, path):
     sc = lib.aiImportFile(path.encode(), FLAGS)
@@ -331,15 +362,18 @@ def main():
     lib.aiGetMaterialString.argtypes = [C.c_void_p, C.c_char_p, C.c_uint, C.c_uint, C.POINTER(AiString)]
     lib.aiGetErrorString.restype = C.c_char_p
     with tempfile.TemporaryDirectory() as d:
-        with open(os.path.join(d, "scene.mtl"), "w") as f:
-            f.write(MTL)
-        for name, text in CASES.items():
+        cases = [(n, t, MTL) for n, t in CASES.items()]
+        if os.path.exists(REF_MTL):
+            cases.append(("nanosuit", NANO_OBJ, open(REF_MTL).read()))
+        for name, text, mtl in cases:
+            with open(os.path.join(d, "scene.mtl"), "w") as f:
+                f.write(mtl)
             p = os.path.join(d, name + ".obj")
             with open(p, "w") as f:
                 f.write(text)
             out = import_with_assimp(lib, p)
             out["obj"] = np.frombuffer(text.encode(), np.uint8)
-            out["mtl"] = np.frombuffer(MTL.encode(), np.uint8)
+            out["mtl"] = np.frombuffer(mtl.encode(), np.uint8)
             np.savez_compressed(os.path.join(HERE, "obj_%s.npz" % name), **out)
             print(name, "meshes", int(out["n_meshes"]),
                   "verts", sum(out["mesh%d_verts" % i].shape[0] for i in range(int(out["n_meshes"]))))
