@@ -136,7 +136,7 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     gb = [torch.from_numpy(a).to(dev) for a in (pos, nrm, alb)]
     ref = O.trace(n, g0, E, ctx.download_level(0), gpu_pyramid_flat(ctx), pos, nrm, alb, cam.position)
-    for variant in (0, 1, 2):
+    for variant in (0, 1, 2, 3):
         d = torch.empty((h, w, 4), device=dev)
         sp = torch.empty((h, w, 4), device=dev)
         st = torch.zeros((h, w), dtype=torch.int32, device=dev)

@@ -675,7 +675,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
 // ===========================================================================
 // the kernel: pixel setup, cone loop, outputs (BRICK = variant 0, else 1)
 // ===========================================================================
-template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2>
+template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true>
 __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
     __shared__ float4 lds_all[BRICK ? 4 : 1][BRICK ? 2 * kEntrySlots : 1];
     // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid
@@ -687,8 +687,12 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
     float4* lds = lds_all[BRICK ? wave : 0];
     PhaseClock pc;
     pc.start();
-    const uint32_t px = (sub & 3) * 16 + (wave & 1) * 8 + (lane & 7);
-    const uint32_t py = (sub >> 2) * 16 + (wave >> 1) * 8 + (lane >> 3);
+    // lane -> pixel of the wave's 8x8 block in Morton order (MORTON; else row-major):
+    // the lanes of each ds_read_b128 / load group are then a compact 2x2 / 4x4 pixel block
+    const uint32_t mx = MORTON ? (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4) : lane & 7;
+    const uint32_t my = MORTON ? ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4) : lane >> 3;
+    const uint32_t px = (sub & 3) * 16 + (wave & 1) * 8 + mx;
+    const uint32_t py = (sub >> 2) * 16 + (wave >> 1) * 8 + my;
     const uint32_t tile = lt * (uint32_t)k.world + (uint32_t)k.rank;
     const uint32_t x = (tile % (uint32_t)k.tiles_x) * VCT_TILE + px;
     const uint32_t y = (tile / (uint32_t)k.tiles_x) * VCT_TILE + py;
@@ -829,6 +833,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers; 2 bricks without the four-face union
         case 1: VCT_K4(false, 1, true); break;
         case 2: VCT_K4(true, VCT_K4_MIN_WAVES, false); break;
+        case 3: hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false>), dim3(blocks), dim3(256), 0, c->stream, k); break;   // row-major lanes
         default: VCT_K4(true, VCT_K4_MIN_WAVES, true);
     }
 #undef VCT_K4
