@@ -338,22 +338,14 @@ struct BrickEntry {
     int lvl;                     // staged level (-1 = empty)
     int ox, oy, oz;              // its origin
 };
-struct BrickCache {              // wave-uniform; two named entries (a runtime-indexed array would live in scratch)
-    BrickEntry e0, e1;
-    __device__ BrickEntry get(int e) const {
-        BrickEntry b;
-        b.lvl = e ? e1.lvl : e0.lvl;
-        b.ox = e ? e1.ox : e0.ox;
-        b.oy = e ? e1.oy : e0.oy;
-        b.oz = e ? e1.oz : e0.oz;
-        return b;
-    }
-    __device__ void set(int e, const BrickEntry& v) {
-        e0.lvl = e ? e0.lvl : v.lvl; e1.lvl = e ? v.lvl : e1.lvl;
-        e0.ox = e ? e0.ox : v.ox; e1.ox = e ? v.ox : e1.ox;
-        e0.oy = e ? e0.oy : v.oy; e1.oy = e ? v.oy : e1.oy;
-        e0.oz = e ? e0.oz : v.oz; e1.oz = e ? v.oz : e1.oz;
-    }
+// The cache holds the bricks of the step's two levels: `a` for level l0, `b`
+// for l0 + 1.  A cone's mip level never decreases, so when l0 advances by one
+// the old `b` becomes the new `a` (the two swap, with their LDS regions) and
+// `b` restages; no per-step indexing (a runtime-indexed pair would cost
+// scalar selects on every access).
+struct BrickCache {              // wave-uniform
+    BrickEntry a, b;
+    int flip;                    // 0: a in LDS region 0, b in region 1; 1: swapped
 };
 
 struct Corner {                  // one lane's trilinear footprint at one level
@@ -503,12 +495,17 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const int modeA = (l0 == 0 || !k.aniso) ? kIso : aniso_mode;
     const int modeB = k.aniso ? aniso_mode : kIso;
     const bool faces_ok = UNION ? cc.nfaces <= 4 : cc.nfaces == 3;
-    const int eA = l0 & 1, eB = eA ^ 1;
-    float4* ldsA = lds + eA * kEntrySlots;
-    float4* ldsB = lds + eB * kEntrySlots;
+    if (bc.a.lvl != l0 && bc.b.lvl == l0) {       // the level advanced by one: b becomes a
+        const BrickEntry t = bc.a;
+        bc.a = bc.b;
+        bc.b = t;
+        bc.flip ^= 1;
+    }
+    float4* ldsA = lds + bc.flip * kEntrySlots;
+    float4* ldsB = lds + (bc.flip ^ 1) * kEntrySlots;
     // level A: cached, restaged, or gathered
     const Corner cA = level_corner(l0, qx, qy, qz);
-    BrickEntry bA = bc.get(eA);
+    BrickEntry bA = bc.a;
     bool useA = bA.lvl == l0 && wall_in(amA, in_brick(cA, bA));
     bool stA = false;
     if (!useA && (modeA != kFaces || faces_ok)) {
@@ -516,12 +513,12 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         nb.lvl = l0;
         if (brick_origin(cA, amA, nb)) {
             bA = nb;
-            bc.set(eA, nb);
+            bc.a = nb;
             useA = stA = true;
         }
     }
     Corner cB = cA;
-    BrickEntry bB = bc.get(eB);
+    BrickEntry bB = bc.b;
     bool useB = false, stB = false;
     if (needB) {
         cB = level_corner(l1, qx, qy, qz);
@@ -531,7 +528,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
             nb.lvl = l1;
             if (brick_origin(cB, amB, nb)) {
                 bB = nb;
-                bc.set(eB, nb);
+                bc.b = nb;
                 useB = stB = true;
             }
         }
@@ -621,7 +618,8 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.dir_uniform = wall_in(vm, (wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz)) && cc.nfaces == 3;
     }
     BrickCache bc;
-    bc.e0 = bc.e1 = BrickEntry{-1, 0, 0, 0};
+    bc.a = bc.b = BrickEntry{-1, 0, 0, 0};
+    bc.flip = 0;
     for (int i = 0;; ++i) {
         float D, fr;
         int l0;
