@@ -331,6 +331,7 @@ struct ConeCtl {                 // wave-uniform facts about one cone
     int nfaces;                  // popcount(funion)
     int f0, f1, f2, f3;          // the faces of funion in increasing order (first nfaces valid)
     bool dir_uniform;            // every valid lane has the same wd = d^2 (bitwise) and the same faces
+    int neg;                     // bit a: every valid lane moves toward -axis a (brick slack goes there)
     float uwx, uwy, uwz;         // that wd
 };
 
@@ -369,20 +370,25 @@ __device__ __forceinline__ bool in_brick(const Corner& c, const BrickEntry& b) {
 
 // Brick origin on one axis without a 64-lane reduction: relative to the first
 // active lane's corner b, the wave fits only if every active lane is within
-// [b-2, b+2]; two ballots then give the minimum exactly (-2, -1 or 0).
-__device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl) {
+// [b-2, b+2]; two ballots then give the minimum (or maximum) exactly.  The
+// brick's slack (3 - span corners) is put ahead of the march: origin = min
+// when the cone moves toward +axis, max - 2 when it moves toward -axis (neg),
+// so the following steps stay inside longer.
+__device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl, bool neg) {
     const int b = __builtin_amdgcn_readlane(v, fl);
-    const int d = v - b;
+    const int d = neg ? b - v : v - b;
     const unsigned long long m2 = wballot(d < -1) & am, m1 = wballot(d < 0) & am;   // m2 within m1
-    return b - (int)(m1 != 0ull) - (int)(m2 != 0ull);
+    const int cnt = (int)(m1 != 0ull) + (int)(m2 != 0ull);
+    return neg ? b + cnt - 2 : b - cnt;
 }
 
-// the per-axis minimum corner over the lanes of am, if every footprint fits the brick there
-__device__ __forceinline__ bool brick_origin(const Corner& c, unsigned long long am, BrickEntry& b) {
+// a brick origin over the lanes of am (neg: bit a = the cone moves toward -axis a),
+// if every footprint fits the brick there
+__device__ __forceinline__ bool brick_origin(const Corner& c, unsigned long long am, int neg, BrickEntry& b) {
     const int fl = am ? __builtin_ctzll(am) : 0;
-    b.ox = wave_origin(c.ix, am, fl);
-    b.oy = wave_origin(c.iy, am, fl);
-    b.oz = wave_origin(c.iz, am, fl);
+    b.ox = wave_origin(c.ix, am, fl, neg & 1);
+    b.oy = wave_origin(c.iy, am, fl, neg & 2);
+    b.oz = wave_origin(c.iz, am, fl, neg & 4);
     return wall_in(am, in_brick(c, b));
 }
 
@@ -511,7 +517,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     if (!useA && (modeA != kFaces || faces_ok)) {
         BrickEntry nb;
         nb.lvl = l0;
-        if (brick_origin(cA, amA, nb)) {
+        if (brick_origin(cA, amA, cc.neg, nb)) {
             bA = nb;
             bc.a = nb;
             useA = stA = true;
@@ -526,7 +532,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         if (!useB && (modeB != kFaces || faces_ok)) {
             BrickEntry nb;
             nb.lvl = l1;
-            if (brick_origin(cB, amB, nb)) {
+            if (brick_origin(cB, amB, cc.neg, nb)) {
                 bB = nb;
                 bc.b = nb;
                 useB = stB = true;
@@ -600,6 +606,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
 #pragma unroll
         for (int f = 0; f < 6; ++f) u |= (wballot((fx == f) | (fy == f) | (fz == f)) & vm) ? 1 << f : 0;
         cc.funion = u;
+        cc.neg = ((u & 3) == 2 ? 1 : 0) | ((u & 12) == 8 ? 2 : 0) | ((u & 48) == 32 ? 4 : 0);
         cc.nfaces = __builtin_popcount(u);
         cc.f0 = __builtin_ctz(u | 64);
         u &= u - 1;
