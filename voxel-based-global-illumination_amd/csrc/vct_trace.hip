@@ -193,13 +193,22 @@ __device__ __forceinline__ LevelView<O32> level_view(const TraceK& k, int l) {
     }
 }
 
+// level l differing per lane (per-pixel roughness): 64-bit per-lane base, so no
+// buffer resource (a scalar operand) has to be built from a per-lane value
+__device__ __forceinline__ LevelView<false> level_view_lane(const TraceK& k, int l) {
+    const uint64_t n = (uint64_t)k.n, n3 = n * n * n, F = k.aniso ? 6u : 1u;
+    const uint64_t m = n >> (l > 0 ? l - 1 : 0);
+    const uint64_t off = l == 0 ? 0u : n3 + F * ((n3 - m * m * m) / 7u);
+    return LevelView<false>{k.pyr + off};
+}
+
 // ===========================================================================
 // per-lane gathers (variant 1, and the fallback of variant 0)
 // ===========================================================================
 // D_l(q, d) (A.5): level 0 / isotropic = T_l; anisotropic = faces combined per
 // corner texel, then trilinear.  Zero border: out-of-range corners read as 0
 // (LevelView); fmaf(w, 0, acc) == acc, the spec's zero-border sum.
-template <bool O32>
+template <bool O32, bool UNIF = false>   // UNIF: l is wave-uniform (buffer resource); else per lane
 __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx, float qy, float qz,
                                                int fx, int fy, int fz, float wdx, float wdy, float wdz) {
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
@@ -218,7 +227,10 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
         in[c] = (unsigned)x < (unsigned)nl && (unsigned)y < (unsigned)nl && (unsigned)z < (unsigned)nl;
         idx[c] = (uint32_t)x + (uint32_t)nl * ((uint32_t)y + (uint32_t)nl * (uint32_t)z);
     }
-    const LevelView<O32> lv = level_view<O32>(k, l);
+    const auto lv = [&] {
+        if constexpr (UNIF) return level_view<O32>(k, l);
+        else return level_view_lane(k, l);
+    }();
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (l == 0 || !k.aniso) {
         float4 v[8];
@@ -563,12 +575,12 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     if (!useA) {
         VCT_DBG(4 + (l0 < 10 ? l0 : 10));
         dbg_fallback_reason(cA, active, modeA != kFaces || faces_ok, l0);
-        if (active) sA = sample_level<O32>(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+        if (active) sA = sample_level<O32, true>(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
     }
     if (needB && !useB) {
         VCT_DBG(4 + (l1 < 10 ? l1 : 10));
         dbg_fallback_reason(cB, activeB, modeB != kFaces || faces_ok, l1);
-        if (activeB) sB = sample_level<O32>(k, l1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+        if (activeB) sB = sample_level<O32, true>(k, l1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
     }
     pc.mark(4);
     return activeB ? blend(sA, sB, fr) : sA;
