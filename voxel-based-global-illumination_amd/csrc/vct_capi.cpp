@@ -145,6 +145,10 @@ vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
         if (e == hipSuccess) e = hipMalloc((void**)&c->step_tab, sizeof rows);
         if (e == hipSuccess) e = hipMemcpy(c->step_tab, rows, sizeof rows, hipMemcpyHostToDevice);
     }
+    if (e == hipSuccess) e = hipMalloc((void**)&c->spec_keys, 2 * kSpecSlots * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(c->spec_keys, 0xff, kSpecSlots * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(c->spec_keys + kSpecSlots, 0, kSpecSlots * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->spec_rows, kSpecSlots * 64 * sizeof(StepRow));
     if (e != hipSuccess) {
         vct_destroy(c);
         return e == hipErrorOutOfMemory ? VCT_ENOMEM : VCT_EDEVICE;
@@ -166,6 +170,8 @@ void vct_destroy(vct_ctx* c) {
     if (g.accum) (void)hipFree(g.accum);
     if (c->mesh.tri) (void)hipFree(c->mesh.tri);
     if (c->step_tab) (void)hipFree(c->step_tab);
+    if (c->spec_keys) (void)hipFree(c->spec_keys);
+    if (c->spec_rows) (void)hipFree(c->spec_rows);
     for (auto& s : c->scratch)
         if (s.p) (void)hipFree(s.p);
     delete c;

@@ -50,6 +50,8 @@ struct vct_ctx {
     vct::Mesh mesh;
     vct::Scratch scratch[4];      // reusable scratch (trace host staging, voxelize temps)
     vct::StepRow* step_tab = nullptr;   // [kMaxStepRows] diffuse-cone step table (device)
+    unsigned* spec_keys = nullptr;      // [2 * kSpecSlots]: specular table keys (~0u free), then states
+    vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)
     std::string err;
 };
 

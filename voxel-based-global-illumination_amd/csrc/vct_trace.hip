@@ -107,6 +107,10 @@ struct TraceK {
     int nd, spec_on, aniso;
     float tau_d;
     const StepRow* steps_tab;    // diffuse-cone step table (tau_d), sentinel-terminated
+    unsigned* spec_keys;         // [kSpecSlots] tau bit patterns of the specular step tables (~0u = free)
+    unsigned* spec_state;        // [kSpecSlots] 0 building, 1 ready, 2 needs more than 64 rows
+    StepRow* spec_rows;          // [kSpecSlots][64]
+    int spec_tabs;               // 0: specular cones always derive their steps per lane (variant bit 0x100)
 };
 
 __device__ __forceinline__ const float (*cone_table(int nd))[4] {
@@ -593,8 +597,67 @@ struct StepRegs {
     int l0;
 };
 
-// one cone, wave-synchronous (A.6); same arithmetic as march().  TAB: the
-// aperture is the diffuse one, (t, D, l0, fr) come from the step table.
+// ---------------------------------------------------------------------------
+// specular step tables: the specular aperture is per pixel (roughness), but a
+// wave whose pixels share one tau can march from a table too.  Tables live in
+// a per-context cache keyed by tau's bit pattern (they depend only on tau, n
+// and L): the first wave that meets a new tau claims a slot, builds the rows
+// (the march() recurrence, lane i keeping row i) and publishes them; later
+// waves, frames and G-buffers only look them up.  A wave that finds the slot
+// still being built, or no free slot, derives (t, D, l0, fr) per lane.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool spec_table(const TraceK& k, float tau, unsigned long long vm, StepRegs& tab) {
+    if (!k.spec_tabs) return false;
+    const int lane = threadIdx.x & 63;
+    const int fl = vm ? __builtin_ctzll(vm) : 0;
+    const float tau0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tau), fl));
+    if (!wall_in(vm, tau == tau0)) return false;
+    const unsigned key = __float_as_uint(tau0);
+    for (int j = 0; j < kSpecSlots; ++j) {
+        unsigned kj = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&k.spec_keys[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (kj == ~0u) {                                        // free: try to claim it for this tau
+            unsigned old = 0;
+            if (lane == 0) old = atomicCAS(&k.spec_keys[j], ~0u, key);
+            old = __builtin_amdgcn_readfirstlane(old);
+            if (old == ~0u) {
+                const float tau2 = 2.0f * tau0, Lf = (float)k.L;
+                float t = 1.0f;
+                StepRow mine{__builtin_inff(), 1.0f, 0.0f, 0};
+                bool fits = false;
+                for (int i = 0; i < 64; ++i) {
+                    if (!(t <= k.tmax)) { fits = true; break; }   // row i stays the sentinel
+                    const float D = fmaxf(1.0f, tau2 * t);
+                    float m = spec_log2(D);
+                    if (m > Lf) m = Lf;
+                    const int l0 = (int)m;
+                    if (lane == i) mine = StepRow{t, D, m - (float)l0, l0};
+                    t = t + VCT_STEP_SCALE * D;
+                }
+                k.spec_rows[j * 64 + lane] = mine;
+                __threadfence();
+                if (lane == 0) __hip_atomic_store(&k.spec_state[j], fits ? 1u : 2u, __ATOMIC_RELEASE,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                if (!fits) return false;
+                tab = StepRegs{mine.t, mine.D, mine.fr, mine.l0};
+                return true;
+            }
+            kj = old;
+        }
+        if (kj == key) {
+            const unsigned st = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&k.spec_state[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
+            if (st != 1u) return false;
+            const StepRow r = k.spec_rows[j * 64 + lane];
+            tab = StepRegs{r.t, r.D, r.fr, r.l0};
+            return true;
+        }
+    }
+    return false;
+}
+
+// one cone, wave-synchronous (A.6); same arithmetic as march().  TAB: (t, D,
+// l0, fr) come from a step table (the diffuse one, or a specular one).
 template <bool O32, bool UNION, bool TAB, int KL>
 __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, float ox, float oy, float oz,
                                                 float dx, float dy, float dz, float tau, float4& res,
@@ -771,8 +834,14 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             if (valid) rough = k.alb[pix].w;
             const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
             float4 res;
-            if constexpr (BRICK) steps += march_brick<O32, UNION, false, KL>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
-            else steps += march<O32>(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
+            if constexpr (BRICK) {
+                if (spec_table(k, tau, wballot(valid), tab))
+                    steps += march_brick<O32, UNION, true, KL>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
+                else
+                    steps += march_brick<O32, UNION, false, KL>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
+            } else {
+                steps += march<O32>(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
+            }
             sout = sel4(valid, res, sout);
         }
     }
@@ -837,6 +906,10 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.aniso = g.aniso;
     k.tau_d = c->cfg.n_diffuse == 16 ? VCT_TAN20 : VCT_TAN30;
     k.steps_tab = c->step_tab;
+    k.spec_keys = c->spec_keys;
+    k.spec_state = c->spec_keys + kSpecSlots;
+    k.spec_rows = c->spec_rows;
+    k.spec_tabs = (a->variant & 0x100) ? 0 : 1;
     const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
     const uint32_t blocks = nlt * 16;
