@@ -11,8 +11,12 @@ assets.cpp:25).
 One "step" = one frame of the cone-trace pass (K4) over the whole framebuffer:
 each rank traces its interleaved 64x64 tiles (tile t -> rank t % N) and, for
 N > 1, the indirect-irradiance + specular framebuffers are all-gathered over
-RCCL and un-permuted on every rank (strong scaling: the frame is fixed, the
-tiles are split).  The level-0 grid is injected on rank 0 and broadcast
+RCCL (one all-gather of the rank's [diffuse | specular] buffer) and
+un-permuted on every rank (strong scaling: the frame is fixed, the tiles are
+split).  Frames are pipelined as a renderer's frame loop would run them: the
+all-gather of frame f overlaps the trace of frame f+1 (vct.multi.FrameTracer);
+every timed step still traces, gathers and un-permutes one whole frame, and
+the pipeline is drained inside the timed region.  The level-0 grid is injected on rank 0 and broadcast
 (RCCL) before the timed region, as when the light changes; K1/K3 timings are
 reported beside the metric.
 
@@ -194,9 +198,8 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         ev[s][0].record(stream)
-        tracer.trace_local(gb, eye, variant=args.variant)
-        ev[s][1].record(stream)
-        tracer.gather()
+        tracer.step(gb, eye, variant=args.variant, on_traced=lambda: ev[s][1].record(stream))
+    tracer.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -134,6 +134,12 @@ uint32_t   vct_tiles_for_rank(uint32_t width, uint32_t height, uint32_t rank, ui
  * max_tiles = vct_tiles_for_rank(w,h,0,world)) into a [h][w][4] frame. */
 vct_status vct_untile_device(vct_ctx* ctx, const float* gathered4, uint32_t width, uint32_t height,
                              uint32_t world, float* frame4);
+/* Several planes in one launch: gathered4 = [world][planes][max_tiles][64*64][4],
+ * i.e. each rank contributed one [planes][max_tiles*64*64][4] buffer (diffuse
+ * and specular side by side, moved by ONE all-gather); plane p is scattered
+ * into frames4[p] (a host array of `planes` device pointers, planes <= 4). */
+vct_status vct_untile_planes_device(vct_ctx* ctx, const float* gathered4, uint32_t planes, uint32_t width,
+                                    uint32_t height, uint32_t world, float* const* frames4);
 
 /* ---- G-buffer (input producer) -----------------------
  * Ray-casts the triangles of the last vct_voxelize call through `cam` into a

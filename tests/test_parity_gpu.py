@@ -211,10 +211,98 @@ def test_tiled_trace_equals_full_frame(gpu_ready, world):
     ctx.untile_device(g_s, w, h, world, fs)
     torch.cuda.synchronize()
     assert torch.equal(fd, full_d) and torch.equal(fs, full_s)
+    # two planes in one launch from the [world][2][max_tiles*64*64][4] layout
+    both = torch.stack([g_d, g_s], 1).contiguous()
+    fd2, fs2 = torch.zeros_like(fd), torch.zeros_like(fs)
+    ctx.untile_planes_device(both, w, h, world, (fd2, fs2))
+    torch.cuda.synchronize()
+    assert torch.equal(fd2, full_d) and torch.equal(fs2, full_s)
     # host mirror of the permutation agrees with the device one
     from vct.multi import untile
     host = untile(g_d.cpu().numpy(), w, h, world)
     assert np.array_equal(host, full_d.cpu().numpy())
+    ctx.close()
+
+
+class _FakeWork:
+    def __init__(self, fn):
+        self.fn = fn
+
+    def wait(self):
+        self.fn()
+
+
+class _FakeGroup:
+    """Stands in for an RCCL group of `world` ranks driven from ONE process: a
+    rank's all_gather_into_tensor is completed when its work is waited on, from
+    every rank's input of the same round (the inputs must still be intact then,
+    which is exactly what FrameTracer's double buffering promises)."""
+
+    def __init__(self, world):
+        self.world, self.inputs, self.round = world, {}, [0] * world
+
+    def view(self, rank):
+        g = self
+
+        class View:
+            def get_backend(self):
+                return "nccl"
+
+            def all_gather_into_tensor(self, out, inp, async_op=False):
+                rd = g.round[rank]
+                g.round[rank] += 1
+                g.inputs[(rd, rank)] = inp
+
+                def done():
+                    for r in range(g.world):
+                        out[r].copy_(g.inputs[(rd, r)])
+                if not async_op:
+                    done()
+                    return None
+                return _FakeWork(done)
+        return View()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_frame_pipeline_equals_full_frames(gpu_ready, world):
+    """FrameTracer (bench.py's per-rank driver): the pipelined step()/drain() loop
+    (all-gather of frame f overlapping the trace of frame f+1, two buffer sets,
+    one [diffuse | specular] gather, one two-plane untile) yields every frame
+    bit-identical to a single-rank trace of it.  Ranks are FrameTracers in one
+    process over a fake group; each frame uses a different eye (specular changes)."""
+    import torch
+    from vct import scenes
+    from vct.camera import Camera
+    from vct.multi import FrameTracer
+    ctx, s, arrs, (g0, E) = gpu_pipeline(32, "atrium")
+    w, h = 200, 130
+    cam = Camera()
+    dev = torch.device("cuda")
+    pos, nrm, alb = (torch.empty((h, w, 4), device=dev) for _ in range(3))
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.gbuffer_raycast_device(cam, w, h, scenes.ROUGHNESS, pos, nrm, alb)
+    eyes = [[float(cam.position[0]) + 0.05 * f, float(cam.position[1]), float(cam.position[2])] for f in range(4)]
+    refs = []
+    for e in eyes:
+        d, sp = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+        ctx.trace_device(pos, nrm, alb, w, h, e, d, sp)
+        refs.append((d, sp))
+    grp = _FakeGroup(world)
+    tr = [FrameTracer(ctx, torch, grp.view(r), w, h, r, world, dev) for r in range(world)]
+    for f, e in enumerate(eyes):
+        for t in tr:
+            t.step((pos, nrm, alb), e)
+        # one rank: the frame is done; several: frame f-1 was completed inside step(f)
+        done = f if world == 1 else f - 1
+        if done >= 0:
+            torch.cuda.synchronize()
+            for t in tr:
+                assert torch.equal(t.diff, refs[done][0]) and torch.equal(t.spec, refs[done][1]), (f, t.rank)
+    for t in tr:
+        t.drain()
+    torch.cuda.synchronize()
+    for t in tr:
+        assert torch.equal(t.diff, refs[-1][0]) and torch.equal(t.spec, refs[-1][1])
     ctx.close()
 
 

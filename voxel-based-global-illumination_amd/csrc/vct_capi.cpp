@@ -343,7 +343,23 @@ vct_status vct_untile_device(vct_ctx* c, const float* gathered4, uint32_t w, uin
     if (!c || !gathered4 || !frame4 || w == 0 || h == 0) return VCT_EINVAL;
     vct_status st = use_device(c);
     if (st != VCT_OK) return st;
-    VCT_HIP(launch_untile(c, (const float4*)gathered4, w, h, world, (float4*)frame4), "untile");
+    float4* f = (float4*)frame4;
+    VCT_HIP(launch_untile(c, (const float4*)gathered4, 1, w, h, world, &f), "untile");
+    return VCT_OK;
+}
+
+vct_status vct_untile_planes_device(vct_ctx* c, const float* gathered4, uint32_t planes, uint32_t w, uint32_t h,
+                                    uint32_t world, float* const* frames4) {
+    if (!c || !gathered4 || !frames4 || w == 0 || h == 0 || planes == 0 || planes > (uint32_t)kMaxUntilePlanes)
+        return VCT_EINVAL;
+    float4* f[kMaxUntilePlanes] = {};
+    for (uint32_t p = 0; p < planes; ++p) {
+        if (!frames4[p]) return VCT_EINVAL;
+        f[p] = (float4*)frames4[p];
+    }
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(launch_untile(c, (const float4*)gathered4, planes, w, h, world, f), "untile planes");
     return VCT_OK;
 }
 

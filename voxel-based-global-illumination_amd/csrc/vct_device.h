@@ -22,7 +22,8 @@ struct StepRow {
     int l0;
 };
 constexpr int kMaxStepRows = 64;   // tan(20 deg) at n = 1024 needs 26 (+1 sentinel)
-constexpr int kSpecSlots = 8;      // specular step tables cached per context (distinct roughness values)
+constexpr int kSpecSlots = 8;
+constexpr int kMaxUntilePlanes = 4;   // vct_untile_planes_device      // specular step tables cached per context (distinct roughness values)
 
 // A.6 mip level m = log2(D), D >= 1 (vct_spec.h VCT_LOG2_*).  Host and device:
 // the host builds K4's step table with it (vct_trace.hip build_step_table).

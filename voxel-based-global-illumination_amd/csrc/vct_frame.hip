@@ -10,17 +10,25 @@
 namespace vct {
 namespace {
 
-// [world][max_tiles][64*64] rank-compact tiles -> [h][w] frame
-__global__ void __launch_bounds__(256) k_untile(const float4* __restrict__ g, int w, int h, int world,
-                                                int tiles_x, int max_tiles, float4* __restrict__ frame) {
+// [world][planes][max_tiles][64*64] rank-compact tiles -> planes x [h][w] frame
+// (blockIdx.z = plane; each rank's planes are contiguous, as one all-gather of
+// the rank's [planes][max_tiles*64*64] buffer lays them out)
+struct UntileK {
+    const float4* g;
+    float4* frame[kMaxUntilePlanes];
+    int w, h, world, tiles_x, max_tiles, planes;
+};
+
+__global__ void __launch_bounds__(256) k_untile(const UntileK k) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
     const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (x >= w || y >= h) return;
-    const int t = (y / VCT_TILE) * tiles_x + (x / VCT_TILE);
-    const int rank = t % world, lt = t / world;
-    const size_t src = ((size_t)rank * max_tiles + lt) * (VCT_TILE * VCT_TILE) +
+    const int p = blockIdx.z;
+    if (x >= k.w || y >= k.h) return;
+    const int t = (y / VCT_TILE) * k.tiles_x + (x / VCT_TILE);
+    const int rank = t % k.world, lt = t / k.world;
+    const size_t src = (((size_t)rank * k.planes + p) * k.max_tiles + lt) * (VCT_TILE * VCT_TILE) +
                        (size_t)(y % VCT_TILE) * VCT_TILE + (x % VCT_TILE);
-    frame[(size_t)y * w + x] = g[src];
+    k.frame[p][(size_t)y * k.w + x] = k.g[src];
 }
 
 // ---- G-buffer ray caster (input producer for synthetic scenes) -----------
@@ -300,14 +308,17 @@ uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
     return (total - rank + world - 1) / world;
 }
 
-hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t w, uint32_t h, uint32_t world,
-                         float4* frame) {
+hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t planes, uint32_t w, uint32_t h,
+                         uint32_t world, float4* const* frames) {
     if (world == 0) world = 1;
-    const int tiles_x = (int)((w + VCT_TILE - 1) / VCT_TILE);
-    const int max_tiles = (int)tiles_for_rank(w, h, 0, world);
-    dim3 grid((w + 15) / 16, (h + 15) / 16);
-    hipLaunchKernelGGL(k_untile, grid, dim3(256), 0, c->stream, gathered, (int)w, (int)h, (int)world,
-                       tiles_x, max_tiles, frame);
+    UntileK k{};
+    k.g = gathered;
+    for (uint32_t p = 0; p < planes; ++p) k.frame[p] = frames[p];
+    k.w = (int)w; k.h = (int)h; k.world = (int)world; k.planes = (int)planes;
+    k.tiles_x = (int)((w + VCT_TILE - 1) / VCT_TILE);
+    k.max_tiles = (int)tiles_for_rank(w, h, 0, world);
+    dim3 grid((w + 15) / 16, (h + 15) / 16, planes);
+    hipLaunchKernelGGL(k_untile, grid, dim3(256), 0, c->stream, k);
     return hipGetLastError();
 }
 

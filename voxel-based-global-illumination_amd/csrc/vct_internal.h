@@ -67,8 +67,8 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
 hipError_t launch_mips(vct_ctx* c);
 // K4
 hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a);
-hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t w, uint32_t h, uint32_t world,
-                         float4* frame);
+hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t planes, uint32_t w, uint32_t h,
+                         uint32_t world, float4* const* frames);
 // composite + present (row f3)
 hipError_t launch_composite(vct_ctx* c, const float4* pos, const float4* nrm, const float4* alb,
                             const float4* diff, const float4* spec, uint32_t w, uint32_t h, const float l[3],

@@ -175,6 +175,13 @@ class Context:
         self._check(self.lib.vct_untile_device(self.h, ptr(gathered4), width, height, world, ptr(frame4)),
                     "untile_device")
 
+    def untile_planes_device(self, gathered4, width, height, world, frames4):
+        """gathered4: [world][planes][max_tiles*64*64][4]; frames4: sequence of [h][w][4] outputs."""
+        ptr = lambda t: t if isinstance(t, int) else t.data_ptr()
+        arr = (C.c_void_p * len(frames4))(*[ptr(f) for f in frames4])
+        self._check(self.lib.vct_untile_planes_device(self.h, ptr(gathered4), len(frames4), width, height, world,
+                                                      C.cast(arr, C.c_void_p)), "untile_planes_device")
+
     def gbuffer_raycast_device(self, cam, width, height, roughness, pos4, nrm4, alb4):
         c = cam.to_ctypes() if hasattr(cam, "to_ctypes") else cam
         ptr = lambda t: t if isinstance(t, int) else t.data_ptr()

@@ -17,7 +17,7 @@ EXPORTS = (
     "vct_create", "vct_destroy", "vct_last_error", "vct_status_string", "vct_abi_version",
     "vct_get_config", "vct_set_stream", "vct_synchronize", "vct_voxelize",
     "vct_inject_directional", "vct_build_mips", "vct_trace", "vct_trace_device",
-    "vct_tiles_for_rank", "vct_untile_device", "vct_gbuffer_raycast_device", "vct_gbuffer_raster_device",
+    "vct_tiles_for_rank", "vct_untile_device", "vct_untile_planes_device", "vct_gbuffer_raycast_device", "vct_gbuffer_raster_device",
     "vct_composite_device",
     "vct_num_levels", "vct_level_dims", "vct_download_level", "vct_upload_level0",
     "vct_level0_device", "vct_copy_level0_to_device", "vct_set_level0_from_device",
@@ -102,6 +102,7 @@ def load() -> C.CDLL:
         "vct_trace_device": (i32, [P, C.POINTER(VctTraceArgs)]),
         "vct_tiles_for_rank": (u32, [u32, u32, u32, u32]),
         "vct_untile_device": (i32, [P, P, u32, u32, u32, P]),
+        "vct_untile_planes_device": (i32, [P, P, u32, u32, u32, u32, P]),
         "vct_gbuffer_raycast_device": (i32, [P, C.POINTER(VctCamera), u32, u32, f32, P, P, P]),
         "vct_gbuffer_raster_device": (i32, [P, C.POINTER(VctCamera), u32, u32, f32, P, P, P]),
         "vct_composite_device": (i32, [P, P, P, P, P, P, u32, u32, C.POINTER(f32), C.POINTER(f32), P, P]),

@@ -68,43 +68,92 @@ def untile(gathered: np.ndarray, w: int, h: int, world: int) -> np.ndarray:
 
 
 class FrameTracer:
-    """Per-rank K4 driver: trace own tiles, all-gather, un-permute (torch + RCCL)."""
+    """Per-rank K4 driver: trace own tiles, all-gather, un-permute (torch + RCCL).
+
+    Each rank traces its tiles into one rank-compact buffer holding the diffuse
+    and the specular plane side by side ([2][max_tiles*64*64][4]), so ONE
+    all-gather moves both; one vct_untile_planes_device launch scatters them.
+    With one rank there is nothing to exchange: the trace writes the frame.
+
+    :meth:`frame` is one synchronous frame.  :meth:`step` / :meth:`drain` run
+    frames as a pipeline (RCCL only): the all-gather of frame f runs on the
+    process group's stream while frame f+1 is traced, and frame f is
+    un-permuted after that trace was queued.  Two buffer sets alternate; the
+    stream order (trace f+1, wait gather f, untile f, trace f+2, ...) keeps a
+    buffer from being overwritten before its gather and untile have read it.
+    """
 
     def __init__(self, ctx, torch, dist, w: int, h: int, rank: int, world: int, device):
         self.ctx, self.torch, self.dist = ctx, torch, dist
         self.w, self.h, self.rank, self.world = w, h, rank, world
         self.max_tiles = tiles_for_rank(w, h, 0, world)
-        npx = self.max_tiles * TILE * TILE
+        self.npx = self.max_tiles * TILE * TILE
         f32 = torch.float32
-        self.diff_c = torch.zeros((npx, 4), dtype=f32, device=device)
-        self.spec_c = torch.zeros((npx, 4), dtype=f32, device=device)
-        if world > 1:
-            self.diff_g = torch.empty((world * npx, 4), dtype=f32, device=device)
-            self.spec_g = torch.empty((world * npx, 4), dtype=f32, device=device)
-        self.diff = torch.empty((h, w, 4), dtype=f32, device=device)
-        self.spec = torch.empty((h, w, 4), dtype=f32, device=device)
+        nsets = 2 if world > 1 else 1
+        self.comp = [torch.zeros((2, self.npx, 4), dtype=f32, device=device) for _ in range(nsets)]
+        self.gath = [torch.empty((world, 2, self.npx, 4), dtype=f32, device=device) for _ in range(nsets)] \
+            if world > 1 else []
+        self.diff = torch.zeros((h, w, 4), dtype=f32, device=device)
+        self.spec = torch.zeros((h, w, 4), dtype=f32, device=device)
+        self.cur = 0
+        self.pending = None
 
-    def trace_local(self, gb, eye, cone_steps=None, texel_fetches=None, steps_px=None, variant=0):
+    def trace_local(self, gb, eye, cone_steps=None, texel_fetches=None, steps_px=None, variant=0, buf=0):
         pos, nrm, alb = gb
-        self.ctx.trace_device(pos, nrm, alb, self.w, self.h, eye, self.diff_c, self.spec_c,
+        if self.world == 1:      # the whole frame: straight into the outputs
+            self.ctx.trace_device(pos, nrm, alb, self.w, self.h, eye, self.diff, self.spec,
+                                  steps_px=steps_px, cone_steps=cone_steps, texel_fetches=texel_fetches,
+                                  variant=variant)
+            return
+        c = self.comp[buf]
+        self.ctx.trace_device(pos, nrm, alb, self.w, self.h, eye, c[0], c[1],
                               steps_px=steps_px, cone_steps=cone_steps, texel_fetches=texel_fetches,
                               tile_rank=self.rank, tile_world=self.world, tile_compact=True, variant=variant)
 
-    def gather(self):
+    def _pipelined(self):
+        return self.world > 1 and self.dist.get_backend() == "nccl"
+
+    def _gather(self, buf, async_op):
+        if self.dist.get_backend() == "nccl":            # RCCL over xGMI
+            return self.dist.all_gather_into_tensor(self.gath[buf], self.comp[buf], async_op=async_op)
+        # gloo (CPU-side rehearsal of the same path)
+        self.dist.all_gather(list(self.gath[buf].unbind(0)), self.comp[buf])
+        return None
+
+    def _untile(self, buf):
+        self.ctx.untile_planes_device(self.gath[buf], self.w, self.h, self.world, (self.diff, self.spec))
+
+    def gather(self, buf=0):
         if self.world > 1:
-            if self.dist.get_backend() == "nccl":          # RCCL over xGMI
-                self.dist.all_gather_into_tensor(self.diff_g, self.diff_c)
-                self.dist.all_gather_into_tensor(self.spec_g, self.spec_c)
-            else:                                          # gloo (CPU-side rehearsal of the same path)
-                self.dist.all_gather(list(self.diff_g.chunk(self.world)), self.diff_c)
-                self.dist.all_gather(list(self.spec_g.chunk(self.world)), self.spec_c)
-            src_d, src_s = self.diff_g, self.spec_g
-        else:
-            src_d, src_s = self.diff_c, self.spec_c
-        self.ctx.untile_device(src_d, self.w, self.h, self.world, self.diff)
-        self.ctx.untile_device(src_s, self.w, self.h, self.world, self.spec)
+            self._gather(buf, False)
+            self._untile(buf)
 
     def frame(self, gb, eye, variant=0):
+        self.drain()
         self.trace_local(gb, eye, variant=variant)
         self.gather()
         return self.diff, self.spec
+
+    def step(self, gb, eye, variant=0, on_traced=None):
+        """One frame of the pipeline; the frame's outputs are complete after the next step() or drain()."""
+        if not self._pipelined():
+            self.trace_local(gb, eye, variant=variant)
+            if on_traced:
+                on_traced()
+            self.gather()
+            return
+        b = self.cur
+        self.cur ^= 1
+        self.trace_local(gb, eye, variant=variant, buf=b)
+        if on_traced:
+            on_traced()
+        work = self._gather(b, True)
+        self.drain()
+        self.pending = (work, b)
+
+    def drain(self):
+        if self.pending is not None:
+            work, b = self.pending
+            self.pending = None
+            work.wait()                                     # current stream waits for the gather
+            self._untile(b)
