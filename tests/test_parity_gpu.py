@@ -126,7 +126,10 @@ def test_trace_parity(gpu_ready, oracle_mod, name, n, kind, aniso, nd, spec):
 @pytest.mark.parametrize("kind", ["scene", "rand", "mirror", "jitter"])
 def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
     """The K4 variants (0 = LDS bricks, 1 = per-lane gathers, 2 = bricks without
-    the four-face union) equal the oracle bit for bit."""
+    the four-face union, 3 = row-major lanes; bit 0x100 = no specular step tables,
+    0x200 = diffuse and specular cones in one workgroup) equal the oracle bit for
+    bit.  Without per-pixel step counts the default splits the diffuse and the
+    specular cones over two workgroups; that form is checked as well."""
     import torch
     O = oracle_mod
     n, w, h = 64, 160, 96
@@ -149,6 +152,15 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         assert np.array_equal(st.cpu().numpy().astype(np.uint32), ref["steps_px"])
         assert int(cnt[0]) == ref["cone_steps"]
         assert int(cnt[1]) > 24 * int(cnt[0]) // 2   # >= 1 aniso level per step on average
+    for variant in (0, 1, 0x100, 0x200):
+        d = torch.full((h, w, 4), -1.0, device=dev)
+        sp = torch.full((h, w, 4), -1.0, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        ctx.trace_device(*gb, w, h, cam.position, d, sp, cone_steps=cnt, variant=variant)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), ref["diffuse"]), f"variant {variant:#x} diffuse (no steps_px)"
+        assert np.array_equal(sp.cpu().numpy(), ref["spec"]), f"variant {variant:#x} spec (no steps_px)"
+        assert int(cnt[0]) == ref["cone_steps"]
     ctx.close()
 
 

@@ -52,6 +52,7 @@ def main():
     d = torch.empty((a.h, a.w, 4), device=dev)
     sp = torch.empty((a.h, a.w, 4), device=dev)
     for v in [int(x, 0) for x in a.variants.split(",")]:
+        ctx.trace_device(*gb, a.w, a.h, cam.position, d, sp, variant=v)   # warm caches, step tables
         torch.cuda.synchronize()
         lib.vct_debug_counters(ctr, 1)
         ctx.trace_device(*gb, a.w, a.h, cam.position, d, sp, variant=v)
@@ -63,6 +64,16 @@ def main():
         print(f"  level A adaptive {c[26]}; level B staged {c[27]} / adaptive {c[28]} / hit {c[29]} / gather {c[30]}")
         print(f"  gather reasons: faces not uniform {c[16]}; footprint span (level 0) <=3/<=5/<=9/more {c[18:22]}"
               f"; (level>0) {c[22:26]}")
+        if a.clk:
+            print(f"  longest wave {c[39]} cycles; wave durations (2^k cycles: count):",
+                  ", ".join(f"{10 + k}:{c[k]}" for k in range(22) if c[k]))
+            lt = max(c[30], 1)
+            nmid = sum(c[8:10])
+            print(f"  waves >= 2^20 cycles: {c[22]}, {c[23] / max(c[22], 1):.0f} steps each; "
+                  f"waves 2^18..2^20: {nmid}, {c[31] / max(nmid, 1):.0f} steps each")
+            print("  waves >= 2^20 cycles, phase split:",
+                  ", ".join(f"{n} {100.0 * c[24 + i] / lt:.1f}%" for i, n in
+                            enumerate(["head", "geometry", "staging", "lds-sample", "fallback", "tail"])))
         names = ["head", "geometry", "staging", "lds-sample", "fallback", "tail", "kernel"]
         tot = max(c[32 + 6], 1)
         print("  phase cycles (sum over waves):",

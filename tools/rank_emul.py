@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Per-rank K4 time of the N-GPU screen-tile split, measured on ONE GPU.
+
+    python tools/rank_emul.py [--worlds 1,2,4,8] [--reps 7] [--n 256 --w 1920 --h 1080]
+
+For each world size N and each rank r < N, times exactly the launch rank r
+makes in the N-GPU bench (its interleaved 64x64 tiles, rank-compact output) and
+reports the slowest rank: the K4 part of the N-GPU step (the all-gather and
+the untile come on top; the gather overlaps the next frame's trace).
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "voxel-based-global-illumination_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--w", type=int, default=1920)
+    ap.add_argument("--h", type=int, default=1080)
+    ap.add_argument("--variant", type=int, default=0)
+    a = ap.parse_args()
+    import torch
+    from vct import Context, scenes
+    from vct.camera import Camera
+    from vct.multi import TILE, tiles_for_rank
+    g0, E = scenes.grid_for_unit_box(a.n)
+    ctx = Context(a.n, g0, E)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+    ctx.voxelize(*scenes.SCENES["atrium"]().arrays())
+    ctx.inject_directional(scenes.LIGHT_DIR)
+    ctx.build_mips()
+    dev = torch.device("cuda")
+    cam = Camera()
+    gb = [torch.empty((a.h, a.w, 4), device=dev) for _ in range(3)]
+    ctx.gbuffer_raycast_device(cam, a.w, a.h, scenes.ROUGHNESS, *gb)
+
+    def timed(fn):
+        ts = []
+        fn()
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return sorted(ts)[len(ts) // 2]
+
+    out = {}
+    for W in [int(x) for x in a.worlds.split(",")]:
+        maxt = tiles_for_rank(a.w, a.h, 0, W)
+        buf = torch.empty((2, maxt * TILE * TILE, 4), device=dev)
+        per = []
+        for r in range(W):
+            per.append(timed(lambda: ctx.trace_device(*gb, a.w, a.h, cam.position, buf[0], buf[1], tile_rank=r,
+                                                      tile_world=W, tile_compact=W > 1, variant=a.variant)))
+        gath = torch.empty((W, 2, maxt * TILE * TILE, 4), device=dev)
+        fr = (torch.empty((a.h, a.w, 4), device=dev), torch.empty((a.h, a.w, 4), device=dev))
+        unt = timed(lambda: ctx.untile_planes_device(gath, a.w, a.h, W, fr)) if W > 1 else 0.0
+        out[W] = {"k4_ms_max_rank": round(max(per), 4), "k4_ms_min_rank": round(min(per), 4),
+                  "tiles_per_rank": maxt, "untile_ms": round(unt, 4)}
+    base = out.get(1, {}).get("k4_ms_max_rank")
+    if base:
+        for W, d in out.items():
+            d["k4_speedup"] = round(base / d["k4_ms_max_rank"], 2)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -56,16 +56,29 @@ __device__ unsigned long long vct_dbg_time[8];
 struct PhaseClock {
 #ifdef VCT_DEBUG_CLOCK
     unsigned long long acc[7] = {}, last = 0, first = 0;
+    unsigned nsteps = 0;
     __device__ void start() { first = last = __builtin_amdgcn_s_memtime(); }
     __device__ void mark(int i) {
         const unsigned long long t = __builtin_amdgcn_s_memtime();
         acc[i] += t - last;
         last = t;
+        nsteps += i == 0;
     }
     __device__ void flush() {
         acc[6] = __builtin_amdgcn_s_memtime() - first;
-        if ((threadIdx.x & 63) == 0)
+        if ((threadIdx.x & 63) == 0) {
             for (int i = 0; i < 7; ++i) atomicAdd(&vct_dbg_time[i], acc[i]);
+            atomicMax(&vct_dbg_time[7], acc[6]);          // longest wave
+            const int lg = 63 - __builtin_clzll(acc[6] | 1);   // wave-duration histogram, 2^(10+k) cycles
+            atomicAdd(&vct_dbg_ctr[lg < 10 ? 0 : (lg > 31 ? 21 : lg - 10)], 1ull);
+            if (lg >= 20) {                                     // phase split of the long waves
+                for (int i = 0; i < 7; ++i) atomicAdd(&vct_dbg_ctr[24 + i], acc[i]);
+                atomicAdd(&vct_dbg_ctr[22], 1ull);
+                atomicAdd(&vct_dbg_ctr[23], (unsigned long long)nsteps);
+            } else if (lg >= 18) {
+                atomicAdd(&vct_dbg_ctr[31], (unsigned long long)nsteps);
+            }
+        }
     }
 #else
     __device__ void start() {}
@@ -111,6 +124,7 @@ struct TraceK {
     unsigned* spec_state;        // [kSpecSlots] 0 building, 1 ready, 2 needs more than 64 rows
     StepRow* spec_rows;          // [kSpecSlots][64]
     int spec_tabs;               // 0: specular cones always derive their steps per lane (variant bit 0x100)
+    int split;                   // 1: two workgroups per 16x16 block, one traces the diffuse cones, one the specular
 };
 
 __device__ __forceinline__ const float (*cone_table(int nd))[4] {
@@ -758,11 +772,20 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
 template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true>
 __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
     __shared__ float4 lds_all[BRICK ? 4 : 1][BRICK ? 2 * kEntrySlots : 1];
+    // split: the grid is two halves over the same pixels, the first traces the
+    // diffuse cones (role 0), the second the specular cone (role 1).  Workgroups
+    // are dispatched in blockIdx order, so the specular half fills the machine as
+    // the diffuse half drains; the halves are multiples of 8 blocks, so a block's
+    // two roles run on the same XCD (same L2).  Shorter waves: the last waves of a
+    // launch (the tail when a rank traces few tiles) end sooner.
+    const uint32_t nb = k.split ? gridDim.x >> 1 : gridDim.x;
+    const uint32_t role = k.split ? (blockIdx.x >= nb ? 1u : 0u) : 2u;   // 0 diffuse, 1 specular, 2 both
+    const uint32_t b = blockIdx.x - (role == 1u ? nb : 0u);
     // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid
-    const uint32_t nb = gridDim.x, b = blockIdx.x;
     const uint32_t xcd = b & 7, q = nb >> 3, r = nb & 7;
     const uint32_t rb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
     const uint32_t lt = rb >> 4, sub = rb & 15;
+    const bool do_diff = role != 1, do_spec = k.spec_on && role != 0;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4* lds = lds_all[BRICK ? wave : 0];
     PhaseClock pc;
@@ -789,7 +812,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
     // loops (background lanes stage texels); variant 1: only valid lanes trace
     const bool run = BRICK ? wany(valid) : valid;
     StepRegs tab{};
-    if (BRICK && run && lane < (uint32_t)kMaxStepRows) {
+    if (BRICK && run && do_diff && lane < (uint32_t)kMaxStepRows) {
         const StepRow r = k.steps_tab[lane];
         tab = StepRegs{r.t, r.D, r.fr, r.l0};
     }
@@ -808,7 +831,8 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
         const float Bx = kb, By = sgn + (ny * ny) * ka, Bz = -ny;
         const float(*cones)[4] = cone_table(k.nd);
         float ir = 0.0f, ig = 0.0f, ib = 0.0f, occ = 0.0f;
-        for (int c = 0; c < k.nd; ++c) {
+        const int nd = do_diff ? k.nd : 0;
+        for (int c = 0; c < nd; ++c) {
             const float cn = cones[c][0], ct = cones[c][1], cb = cones[c][2], wk = cones[c][3];
             const float dx = (cn * nx + ct * Tx) + cb * Bx;
             const float dy = (cn * ny + ct * Ty) + cb * By;
@@ -822,7 +846,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             occ = fmaf(wk, res.w, occ);
         }
         dout = sel4(valid, make_float4(ir, ig, ib, 1.0f - occ), dout);
-        if (k.spec_on) {
+        if (do_spec) {
             float vx = k.ex - P.x, vy = k.ey - P.y, vz = k.ez - P.z;
             float vl = sqrtf(dot3(vx, vy, vz, vx, vy, vz));
             vl = valid ? vl : 1.0f;
@@ -846,8 +870,8 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
         }
     }
     if (in_frame || k.compact) {
-        k.diff[oidx] = dout;
-        k.spec[oidx] = sout;
+        if (role != 1) k.diff[oidx] = dout;
+        if (role != 0) k.spec[oidx] = sout;
         if (k.steps_px && in_frame) k.steps_px[pix] = steps;
     }
     if (k.steps_total) {
@@ -910,9 +934,12 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.spec_state = c->spec_keys + kSpecSlots;
     k.spec_rows = c->spec_rows;
     k.spec_tabs = (a->variant & 0x100) ? 0 : 1;
+    // diffuse / specular roles in separate workgroups (variant bit 0x200 turns it off);
+    // per-pixel step counts need both roles in one lane, so steps_px keeps one role
+    k.split = (k.spec_on && k.nd > 0 && !a->steps_px && !(a->variant & 0x200)) ? 1 : 0;
     const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
-    const uint32_t blocks = nlt * 16;
+    const uint32_t blocks = nlt * 16 * (k.split ? 2u : 1u);
     // O32 instantiations need every level below 4 GiB: n <= 512
     const bool o32 = g.n <= 512;
 #define VCT_K4(BRICK, MINW, UNION)                                                                      \
