@@ -12,6 +12,9 @@
 // result is independent of atomic arrival order: bit-exact and reproducible.
 // Per-voxel accumulators are 64-byte records [albedo rgb, normal xyz, count,
 // pad] so a voxel's seven atomics land in one half cache line.
+#include <algorithm>
+#include <cstdlib>
+
 #include "vct_internal.h"
 
 namespace vct {
@@ -289,6 +292,222 @@ __global__ void __launch_bounds__(256) k1_resolve(const long long* __restrict__ 
 }
 
 // ---- K2 injection ----------------------------------------------------------
+// Work-list form (default):
+//   k2_list    occupied voxels from the level-0 occupancy bits (a wave takes 64
+//              words; per word, lane j owns bit j: ballot + mbcnt give coalesced
+//              slots, one atomic per wave);
+//   k2_shade   per occupied voxel: n.l <= 0 -> (0,0,0,1) now, else onto the lit list;
+//   k2_coarse  one bit per (n/64)^3 brick (64^3 bits = 32 KiB);
+//   k2_walk    per lit voxel the A.3 shadow walk, with the coarse bits in LDS: a
+//              voxel of an empty brick is empty, so its fine word is not read
+//              (same cells, same float sequence, same result).
+// Level 0 is zeroed first; every voxel's value depends on that voxel alone, so
+// the list order (waves append in any order) does not change the output.
+// exclusive prefix sum of one value per thread over a 256-thread block, and the
+// block total (4 waves: shuffles within the wave, wave totals through LDS)
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t& total) {
+    __shared__ uint32_t wt[4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl += t;
+    }
+    if (lane == 63) wt[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += wt[w];
+    total = wt[0] + wt[1] + wt[2] + wt[3];
+    __syncthreads();
+    return before + incl - v;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// one block = 256 words; entries in bitmask order; one atomic per block
+__global__ void __launch_bounds__(256) k2_list(const unsigned long long* __restrict__ bits, size_t nwords,
+                                               uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+    __shared__ uint32_t s_base;
+    const size_t w = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long mine = w < nwords ? bits[w] : 0ull;
+    uint32_t total;
+    const uint32_t excl = block_excl_scan((uint32_t)__popcll(mine), total);
+    if (total == 0) return;                                  // block-uniform
+    if (threadIdx.x == 0) s_base = atomicAdd(count, total);
+    __syncthreads();
+    const uint32_t base = s_base;
+    const size_t w0 = w - lane;                              // the wave's first word
+    for (int i = 0; i < 64; ++i) {
+        const unsigned long long m =
+            ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), i) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, i);
+        if (m == 0ull) continue;
+        const uint32_t start = base + (uint32_t)__builtin_amdgcn_readlane((int)excl, i);
+        if ((m >> lane) & 1ull) list[start + lanes_below(m)] = (uint32_t)((w0 + i) * 64 + lane);
+    }
+}
+
+// one block = a chunk of 16 x 256 occupied entries: unlit voxels get (0,0,0,1)
+// now, lit ones go onto the lit list in occupied-list order; one atomic per block
+constexpr int kShadeJ = 16;
+__global__ void __launch_bounds__(256) k2_shade(const uint32_t* __restrict__ occ, const uint32_t* __restrict__ n_occ,
+                                                const float4* __restrict__ normal, float lx, float ly, float lz,
+                                                uint32_t* __restrict__ lit, uint32_t* __restrict__ n_lit,
+                                                float4* __restrict__ r0) {
+    __shared__ uint32_t s_cnt[kShadeJ * 4];
+    __shared__ uint32_t s_base;
+    const uint32_t cnt = *n_occ;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t c0 = blockIdx.x * (256 * kShadeJ); c0 < cnt; c0 += gridDim.x * (256 * kShadeJ)) {
+        uint32_t flags = 0, vs[kShadeJ];
+#pragma unroll
+        for (int j = 0; j < kShadeJ; ++j) {
+            const uint32_t i = c0 + j * 256 + threadIdx.x;
+            vs[j] = 0;
+            if (i < cnt) {
+                const uint32_t v = occ[i];
+                const float4 nm = normal[v];
+                const float ndl = dot3(nm.x, nm.y, nm.z, lx, ly, lz);
+                if (ndl > 0.0f) flags |= 1u << j;
+                else r0[v] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+                vs[j] = v;
+            }
+            const unsigned long long b = __ballot((flags >> j) & 1u);
+            if (lane == 0) s_cnt[j * 4 + wave] = (uint32_t)__popcll(b);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = 0;
+            for (int q = 0; q < kShadeJ * 4; ++q) {
+                const uint32_t t = s_cnt[q];
+                s_cnt[q] = run;
+                run += t;
+            }
+            s_base = run ? atomicAdd(n_lit, run) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kShadeJ; ++j) {
+            const unsigned long long b = __ballot((flags >> j) & 1u);
+            if ((flags >> j) & 1u) lit[s_base + s_cnt[j * 4 + wave] + lanes_below(b)] = vs[j];
+        }
+        __syncthreads();
+    }
+}
+
+// coarse occupancy: bit c of brick (bx, by, bz) (brick edge 2^cs) is set when any
+// voxel of it is occupied; cn = n >> cs bricks per axis
+__global__ void __launch_bounds__(256) k2_coarse(const unsigned long long* __restrict__ bits, int n, int cs,
+                                                 uint32_t* __restrict__ coarse) {
+    const int cn = n >> cs;
+    const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t ncb = (uint32_t)cn * cn * cn;
+    bool any = false;
+    if (c < ncb) {
+        const int bx = (int)(c % cn), by = (int)((c / cn) % cn), bz = (int)(c / ((uint32_t)cn * cn));
+        const int e = 1 << cs;
+        for (int z = bz * e; z < bz * e + e && !any; ++z)
+            for (int y = by * e; y < by * e + e && !any; ++y)
+                for (int x = bx * e; x < bx * e + e; x += 64 < e ? 64 : e) {
+                    const size_t v = (size_t)x + (size_t)n * ((size_t)y + (size_t)n * (size_t)z);
+                    const int len = e < 64 ? e : 64;
+                    const unsigned long long m = len == 64 ? ~0ull : ((1ull << len) - 1ull) << (v & 63);
+                    if (bits[v >> 6] & m) { any = true; break; }
+                }
+    }
+    const unsigned long long b = __ballot(any);
+    if (c < ncb && (c & 31) == 0) coarse[c >> 5] = (uint32_t)(b >> (threadIdx.x & 32));
+}
+
+// A.3 shadow walk with the coarse bits (LDS) in front of the fine word: the
+// dda_visibility() sequence, cell for cell
+__device__ __forceinline__ float dda_coarse(const unsigned long long* __restrict__ bits, const uint32_t* __restrict__ cb,
+                                            int N, int cs, int cn, float qx, float qy, float qz, float lx, float ly,
+                                            float lz) {
+    int vx = (int)floorf(qx), vy = (int)floorf(qy), vz = (int)floorf(qz);
+    if (vx < 0 || vy < 0 || vz < 0 || vx >= N || vy >= N || vz >= N) return 1.0f;
+    int sx = lx > 0.0f ? 1 : (lx < 0.0f ? -1 : 0);
+    int sy = ly > 0.0f ? 1 : (ly < 0.0f ? -1 : 0);
+    int sz = lz > 0.0f ? 1 : (lz < 0.0f ? -1 : 0);
+    const float inf = __builtin_inff();
+    float tdx = sx ? 1.0f / fabsf(lx) : inf;
+    float tdy = sy ? 1.0f / fabsf(ly) : inf;
+    float tdz = sz ? 1.0f / fabsf(lz) : inf;
+    float tmx = sx > 0 ? ((float)(vx + 1) - qx) * tdx : (sx < 0 ? (qx - (float)vx) * tdx : inf);
+    float tmy = sy > 0 ? ((float)(vy + 1) - qy) * tdy : (sy < 0 ? (qy - (float)vy) * tdy : inf);
+    float tmz = sz > 0 ? ((float)(vz + 1) - qz) * tdz : (sz < 0 ? (qz - (float)vz) * tdz : inf);
+    // batches of kB cells: the walk itself (integer cells, the float t sequence)
+    // does not depend on the lookups, so a batch's LDS reads are issued together
+    // and its cells then tested in walk order
+    constexpr int kB = 8;
+    for (;;) {
+        uint32_t cv[kB], cc[kB];
+        int nb = 0;
+        bool out = false;
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            if (!out) {
+                cv[b] = (uint32_t)vx + (uint32_t)N * ((uint32_t)vy + (uint32_t)N * (uint32_t)vz);
+                cc[b] = (uint32_t)(vx >> cs) + (uint32_t)cn * ((uint32_t)(vy >> cs) + (uint32_t)cn * (uint32_t)(vz >> cs));
+                ++nb;
+                if (tmx <= tmy && tmx <= tmz) {
+                    vx += sx; out = vx < 0 || vx >= N; tmx = tmx + tdx;
+                } else if (tmy <= tmz) {
+                    vy += sy; out = vy < 0 || vy >= N; tmy = tmy + tdy;
+                } else {
+                    vz += sz; out = vz < 0 || vz >= N; tmz = tmz + tdz;
+                }
+            }
+        }
+        uint32_t hit = 0;
+#pragma unroll
+        for (int b = 0; b < kB; ++b)
+            if (b < nb) hit |= ((cb[cc[b] >> 5] >> (cc[b] & 31)) & 1u) << b;
+        while (hit) {                                   // coarse-occupied cells, in walk order
+            const int b = __builtin_ctz(hit);
+            hit &= hit - 1;
+            uint32_t v = 0;
+#pragma unroll
+            for (int q = 0; q < kB; ++q) v = q == b ? cv[q] : v;
+            if ((bits[v >> 6] >> (v & 63)) & 1ull) return 0.0f;
+        }
+        if (out) return 1.0f;
+    }
+}
+
+constexpr int kCoarseWords = 64 * 64 * 64 / 32;   // 32 KiB of LDS
+
+__global__ void __launch_bounds__(256) k2_walk(const uint32_t* __restrict__ lit, const uint32_t* __restrict__ n_lit,
+                                               const uint32_t* __restrict__ coarse, int cs,
+                                               const float4* __restrict__ albedo_occ,
+                                               const float4* __restrict__ normal,
+                                               const unsigned long long* __restrict__ bits, int n, float lx,
+                                               float ly, float lz, float cr, float cg, float cb,
+                                               float4* __restrict__ r0) {
+    __shared__ uint32_t cbits[kCoarseWords];
+    const int cn = n >> cs;
+    const uint32_t nw = ((uint32_t)cn * cn * cn + 31) / 32;
+    for (uint32_t i = threadIdx.x; i < nw; i += 256) cbits[i] = coarse[i];
+    __syncthreads();
+    const uint32_t cnt = *n_lit;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
+        const uint32_t v = lit[i];
+        const float4 ao = albedo_occ[v];
+        const float4 nm = normal[v];
+        const float ndl = dot3(nm.x, nm.y, nm.z, lx, ly, lz);
+        const int x = (int)(v % (uint32_t)n), y = (int)((v / (uint32_t)n) % (uint32_t)n),
+                  z = (int)(v / ((uint32_t)n * (uint32_t)n));
+        const float vis = dda_coarse(bits, cbits, n, cs, cn, ((float)x + 0.5f) + nm.x, ((float)y + 0.5f) + nm.y,
+                                     ((float)z + 0.5f) + nm.z, lx, ly, lz);
+        r0[v] = make_float4(((ao.x * cr) * ndl) * vis, ((ao.y * cg) * ndl) * vis, ((ao.z * cb) * ndl) * vis, 1.0f);
+    }
+}
+
+// dense form (one lane per voxel), kept for the voxel-parallel A/B (VCT_K2_DENSE)
 __global__ void __launch_bounds__(256) k2_inject(const float4* __restrict__ albedo_occ,
                                                  const float4* __restrict__ normal,
                                                  const unsigned long long* __restrict__ bits, int n,
@@ -372,7 +591,35 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
 hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb) {
     Grid& g = c->grid;
     const size_t nv = (size_t)g.n * g.n * g.n;
-    hipLaunchKernelGGL(k2_inject, dim3((uint32_t)((nv + 255) / 256)), dim3(256), 0, c->stream,
+    if (getenv("VCT_K2_DENSE")) {
+        hipLaunchKernelGGL(k2_inject, dim3((uint32_t)((nv + 255) / 256)), dim3(256), 0, c->stream,
+                           g.albedo_occ, g.normal, g.occ_bits, (int)g.n, lx, ly, lz, cr, cg, cb, g.pyr);
+        return hipGetLastError();
+    }
+    // lists of the occupied and of the lit voxels (n^3 <= 2^30: 32-bit entries),
+    // coarse bits, level 0 zeroed; then one lane per occupied / lit voxel
+    const size_t nwords = nv / 64;
+    int cs = 0;
+    while ((g.n >> cs) > 64) ++cs;
+    const uint32_t cn = g.n >> cs, ncw = (cn * cn * cn + 31) / 32;
+    void* sp = nullptr;
+    hipError_t e = scratch_get(c, 4, 256 + nv * 4 * 2 + (size_t)ncw * 4, &sp);
+    if (e != hipSuccess) return e;
+    uint32_t* counts = (uint32_t*)sp;            // [0] occupied, [1] lit
+    uint32_t* occ = (uint32_t*)((char*)sp + 256);
+    uint32_t* lit = occ + nv;
+    uint32_t* coarse = lit + nv;
+    hipStream_t s = c->stream;
+    if ((e = hipMemsetAsync(counts, 0, 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(g.pyr, 0, nv * sizeof(float4), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k2_list, dim3((uint32_t)((nwords + 255) / 256)), dim3(256), 0, s, g.occ_bits, nwords, occ,
+                       counts);
+    hipLaunchKernelGGL(k2_coarse, dim3((cn * cn * cn + 255) / 256), dim3(256), 0, s, g.occ_bits, (int)g.n, cs,
+                       coarse);
+    const uint32_t blocks = (uint32_t)std::min<size_t>((nv / 64 + 255) / 256 + 1, 4096);
+    hipLaunchKernelGGL(k2_shade, dim3(blocks), dim3(256), 0, s, occ, counts, g.normal, lx, ly, lz, lit, counts + 1,
+                       g.pyr);
+    hipLaunchKernelGGL(k2_walk, dim3(std::min<uint32_t>(blocks, 1024)), dim3(256), 0, s, lit, counts + 1, coarse, cs,
                        g.albedo_occ, g.normal, g.occ_bits, (int)g.n, lx, ly, lz, cr, cg, cb, g.pyr);
     return hipGetLastError();
 }
