@@ -441,60 +441,66 @@ __device__ __forceinline__ float dda_coarse(const unsigned long long* __restrict
     float tmy = sy > 0 ? ((float)(vy + 1) - qy) * tdy : (sy < 0 ? (qy - (float)vy) * tdy : inf);
     float tmz = sz > 0 ? ((float)(vz + 1) - qz) * tdz : (sz < 0 ? (qz - (float)vz) * tdz : inf);
     // batches of kB cells: the walk itself (integer cells, the float t sequence)
-    // does not depend on the lookups, so a batch's LDS reads are issued together
-    // and its cells then tested in walk order
+    // does not depend on the lookups, so a batch's cells are stepped first,
+    // branch-free (selects, no exec-mask branches), then looked up together.
+    // A cell counts only while the walk is inside the grid; any occupied counted
+    // cell blocks the light (the walk stops at the first one either way).
     constexpr int kB = 8;
     for (;;) {
         uint32_t cv[kB], cc[kB];
-        int nb = 0;
+        bool in[kB];
         bool out = false;
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
-            if (!out) {
-                cv[b] = (uint32_t)vx + (uint32_t)N * ((uint32_t)vy + (uint32_t)N * (uint32_t)vz);
-                cc[b] = (uint32_t)(vx >> cs) + (uint32_t)cn * ((uint32_t)(vy >> cs) + (uint32_t)cn * (uint32_t)(vz >> cs));
-                ++nb;
-                if (tmx <= tmy && tmx <= tmz) {
-                    vx += sx; out = vx < 0 || vx >= N; tmx = tmx + tdx;
-                } else if (tmy <= tmz) {
-                    vy += sy; out = vy < 0 || vy >= N; tmy = tmy + tdy;
-                } else {
-                    vz += sz; out = vz < 0 || vz >= N; tmz = tmz + tdz;
-                }
+            in[b] = !out;
+            cv[b] = (uint32_t)vx + (uint32_t)N * ((uint32_t)vy + (uint32_t)N * (uint32_t)vz);
+            cc[b] = (uint32_t)(vx >> cs) + (uint32_t)cn * ((uint32_t)(vy >> cs) + (uint32_t)cn * (uint32_t)(vz >> cs));
+            const bool bx = tmx <= tmy && tmx <= tmz;
+            const bool by = !bx && tmy <= tmz;
+            const bool bz = !bx && !by;
+            const float nx = tmx + tdx, ny = tmy + tdy, nz = tmz + tdz;
+            if (!out) {                                  // freeze the walk once it has left
+                vx += bx ? sx : 0;
+                vy += by ? sy : 0;
+                vz += bz ? sz : 0;
+                tmx = bx ? nx : tmx;
+                tmy = by ? ny : tmy;
+                tmz = bz ? nz : tmz;
+                out = (uint32_t)vx >= (uint32_t)N || (uint32_t)vy >= (uint32_t)N || (uint32_t)vz >= (uint32_t)N;
             }
         }
-        uint32_t hit = 0;
+        bool blocked = false;
+        unsigned long long wd[kB];
 #pragma unroll
-        for (int b = 0; b < kB; ++b)
-            if (b < nb) hit |= ((cb[cc[b] >> 5] >> (cc[b] & 31)) & 1u) << b;
-        while (hit) {                                   // coarse-occupied cells, in walk order
-            const int b = __builtin_ctz(hit);
-            hit &= hit - 1;
-            uint32_t v = 0;
-#pragma unroll
-            for (int q = 0; q < kB; ++q) v = q == b ? cv[q] : v;
-            if ((bits[v >> 6] >> (v & 63)) & 1ull) return 0.0f;
+        for (int b = 0; b < kB; ++b) {
+            const bool co = in[b] && ((cb[in[b] ? cc[b] >> 5 : 0] >> (cc[b] & 31)) & 1u);
+            wd[b] = bits[co ? cv[b] >> 6 : 0];
+            wd[b] = co ? wd[b] : 0ull;
         }
+#pragma unroll
+        for (int b = 0; b < kB; ++b) blocked |= ((wd[b] >> (cv[b] & 63)) & 1ull) != 0ull;
+        if (blocked) return 0.0f;
         if (out) return 1.0f;
     }
 }
 
 constexpr int kCoarseWords = 64 * 64 * 64 / 32;   // 32 KiB of LDS
 
-__global__ void __launch_bounds__(256) k2_walk(const uint32_t* __restrict__ lit, const uint32_t* __restrict__ n_lit,
-                                               const uint32_t* __restrict__ coarse, int cs,
-                                               const float4* __restrict__ albedo_occ,
-                                               const float4* __restrict__ normal,
-                                               const unsigned long long* __restrict__ bits, int n, float lx,
-                                               float ly, float lz, float cr, float cg, float cb,
-                                               float4* __restrict__ r0) {
+// one lane per lit voxel; 1024-thread blocks share one LDS copy of the coarse bits
+__global__ void __launch_bounds__(1024) k2_walk(const uint32_t* __restrict__ lit, const uint32_t* __restrict__ n_lit,
+                                                const uint32_t* __restrict__ coarse, int cs,
+                                                const float4* __restrict__ albedo_occ,
+                                                const float4* __restrict__ normal,
+                                                const unsigned long long* __restrict__ bits, int n, float lx,
+                                                float ly, float lz, float cr, float cg, float cb,
+                                                float4* __restrict__ r0) {
     __shared__ uint32_t cbits[kCoarseWords];
     const int cn = n >> cs;
-    const uint32_t nw = ((uint32_t)cn * cn * cn + 31) / 32;
-    for (uint32_t i = threadIdx.x; i < nw; i += 256) cbits[i] = coarse[i];
+    const uint32_t ncw = ((uint32_t)cn * cn * cn + 31) / 32;
+    for (uint32_t i = threadIdx.x; i < ncw; i += 1024) cbits[i] = coarse[i];
     __syncthreads();
     const uint32_t cnt = *n_lit;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
+    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < cnt; i += gridDim.x * 1024) {
         const uint32_t v = lit[i];
         const float4 ao = albedo_occ[v];
         const float4 nm = normal[v];
@@ -619,7 +625,7 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
     const uint32_t blocks = (uint32_t)std::min<size_t>((nv / 64 + 255) / 256 + 1, 4096);
     hipLaunchKernelGGL(k2_shade, dim3(blocks), dim3(256), 0, s, occ, counts, g.normal, lx, ly, lz, lit, counts + 1,
                        g.pyr);
-    hipLaunchKernelGGL(k2_walk, dim3(std::min<uint32_t>(blocks, 1024)), dim3(256), 0, s, lit, counts + 1, coarse, cs,
+    hipLaunchKernelGGL(k2_walk, dim3(512), dim3(1024), 0, s, lit, counts + 1, coarse, cs,
                        g.albedo_occ, g.normal, g.occ_bits, (int)g.n, lx, ly, lz, cr, cg, cb, g.pyr);
     return hipGetLastError();
 }
