@@ -127,9 +127,11 @@ def test_trace_parity(gpu_ready, oracle_mod, name, n, kind, aniso, nd, spec):
 def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
     """The K4 variants (0 = LDS bricks, 1 = per-lane gathers, 2 = bricks without
     the four-face union, 3 = row-major lanes; bit 0x100 = no specular step tables,
-    0x200 = diffuse and specular cones in one workgroup) equal the oracle bit for
-    bit.  Without per-pixel step counts the default splits the diffuse and the
-    specular cones over two workgroups; that form is checked as well."""
+    0x200 = all cones in one workgroup, 0x400 / 0x800 = cones split over three /
+    two workgroups) equal the oracle bit for bit.  Without per-pixel step counts
+    the default splits the cones over workgroups (three parts for small launches,
+    with a hand-over of the diffuse sum through global scratch); those forms are
+    checked as well, twice in a row (the hand-over flags reset themselves)."""
     import torch
     O = oracle_mod
     n, w, h = 64, 160, 96
@@ -152,7 +154,7 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         assert np.array_equal(st.cpu().numpy().astype(np.uint32), ref["steps_px"])
         assert int(cnt[0]) == ref["cone_steps"]
         assert int(cnt[1]) > 24 * int(cnt[0]) // 2   # >= 1 aniso level per step on average
-    for variant in (0, 1, 0x100, 0x200):
+    for variant in (0, 1, 0x100, 0x200, 0x400, 0x800, 0x400, 0):
         d = torch.full((h, w, 4), -1.0, device=dev)
         sp = torch.full((h, w, 4), -1.0, device=dev)
         cnt = torch.zeros(1, dtype=torch.int64, device=dev)

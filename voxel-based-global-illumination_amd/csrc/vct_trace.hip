@@ -124,7 +124,13 @@ struct TraceK {
     unsigned* spec_state;        // [kSpecSlots] 0 building, 1 ready, 2 needs more than 64 rows
     StepRow* spec_rows;          // [kSpecSlots][64]
     int spec_tabs;               // 0: specular cones always derive their steps per lane (variant bit 0x100)
-    int split;                   // 1: two workgroups per 16x16 block, one traces the diffuse cones, one the specular
+    int split;                   // 0: one workgroup per 16x16 block traces every cone; 1: two (diffuse | specular);
+                                 // 2: three (diffuse cones [0, nd_half) | [nd_half, nd) | specular)
+    int nd_half;
+    float4* sc_part;             // split 2: [px] diffuse sum after cones [0, nd_half)  (per output index)
+    float4* sc_cone;             // split 2: [cone - nd_half][px] results of cones [nd_half, nd)
+    size_t sc_px;                // pixels per scratch plane
+    unsigned* sc_flag;           // split 2: [block][wave] hand-over counter (0 between launches)
 };
 
 __device__ __forceinline__ const float (*cone_table(int nd))[4] {
@@ -766,26 +772,57 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     return steps;
 }
 
+// Hand-over data between the two diffuse parts of split 2: relaxed agent-scope
+// atomic stores / loads (device-coherent sc1 accesses, no L2 write-back or
+// invalidate as a release / acquire fence would issue per wave); the writer
+// waits for its stores before it counts in on the pair's flag.
+__device__ __forceinline__ void st_coherent(float4* p, float4 v) {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    __hip_atomic_store(q + 0, __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, __float_as_uint(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 2, __float_as_uint(v.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 3, __float_as_uint(v.w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float4 ld_coherent(float4* p) {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    return make_float4(__uint_as_float(__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                       __uint_as_float(__hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                       __uint_as_float(__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                       __uint_as_float(__hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
+
 // ===========================================================================
 // the kernel: pixel setup, cone loop, outputs (BRICK = variant 0, else 1)
 // ===========================================================================
-template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true>
-__global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
+template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true, bool S3 = false>
+__global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {   // S3: the split-2 instantiation
     __shared__ float4 lds_all[BRICK ? 4 : 1][BRICK ? 2 * kEntrySlots : 1];
-    // split: the grid is two halves over the same pixels, the first traces the
-    // diffuse cones (role 0), the second the specular cone (role 1).  Workgroups
-    // are dispatched in blockIdx order, so the specular half fills the machine as
-    // the diffuse half drains; the halves are multiples of 8 blocks, so a block's
-    // two roles run on the same XCD (same L2).  Shorter waves: the last waves of a
-    // launch (the tail when a rank traces few tiles) end sooner.
-    const uint32_t nb = k.split ? gridDim.x >> 1 : gridDim.x;
-    const uint32_t role = k.split ? (blockIdx.x >= nb ? 1u : 0u) : 2u;   // 0 diffuse, 1 specular, 2 both
-    const uint32_t b = blockIdx.x - (role == 1u ? nb : 0u);
+    // split: the grid is 2 or 3 parts over the same pixels, dispatched in
+    // blockIdx order: split 1 = diffuse cones | specular cone; split 2 = diffuse
+    // cones [0, nd_half) | [nd_half, nd) | specular.  The parts are multiples of
+    // 8 blocks, so a block's parts run on the same XCD (same L2).  Shorter waves:
+    // the last waves of a launch (the tail when a rank traces few tiles) end
+    // sooner.  In split 2 the two diffuse halves hand over through global
+    // scratch: the first to finish leaves its data, the second completes the
+    // spec's cone-order sum (the same fmaf chain) and writes the output.
+    const uint32_t nb = S3 ? gridDim.x / 3u : (k.split ? gridDim.x >> 1 : gridDim.x);
+    const uint32_t part = blockIdx.x >= nb ? (blockIdx.x >= 2u * nb ? 2u : 1u) : 0u;
+    const uint32_t b = blockIdx.x - part * nb;
     // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid
     const uint32_t xcd = b & 7, q = nb >> 3, r = nb & 7;
     const uint32_t rb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
     const uint32_t lt = rb >> 4, sub = rb & 15;
-    const bool do_diff = role != 1, do_spec = k.spec_on && role != 0;
+    int c_lo = 0, c_hi = k.nd, grp = 0;        // diffuse cones [c_lo, c_hi); grp 1/2: a half of split 2
+    bool do_spec = k.spec_on != 0, wr_diff = true, wr_spec = true;
+    if (k.split == 1) {
+        if (part == 0) { do_spec = false; wr_spec = false; }
+        else { c_hi = 0; wr_diff = false; }
+    } else if (S3) {
+        if (part == 2) { c_hi = 0; wr_diff = false; }
+        else { do_spec = false; wr_spec = false; wr_diff = false; grp = (int)part + 1;
+               if (part == 0) c_hi = k.nd_half; else c_lo = k.nd_half; }
+    }
+    const bool do_diff = c_hi > c_lo;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4* lds = lds_all[BRICK ? wave : 0];
     PhaseClock pc;
@@ -816,6 +853,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
         const StepRow r = k.steps_tab[lane];
         tab = StepRegs{r.t, r.D, r.fr, r.l0};
     }
+    float ir = 0.0f, ig = 0.0f, ib = 0.0f, occ = 0.0f;   // diffuse sum in cone order
     if (run) {
         float4 N4 = make_float4(0.0f, 1.0f, 0.0f, 0.0f);
         if (valid) N4 = k.nrm[pix];
@@ -830,9 +868,7 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
         const float Tx = 1.0f + ((sgn * nx) * nx) * ka, Ty = sgn * kb, Tz = -(sgn * nx);
         const float Bx = kb, By = sgn + (ny * ny) * ka, Bz = -ny;
         const float(*cones)[4] = cone_table(k.nd);
-        float ir = 0.0f, ig = 0.0f, ib = 0.0f, occ = 0.0f;
-        const int nd = do_diff ? k.nd : 0;
-        for (int c = 0; c < nd; ++c) {
+        for (int c = S3 ? c_lo : 0; c < c_hi; ++c) {
             const float cn = cones[c][0], ct = cones[c][1], cb = cones[c][2], wk = cones[c][3];
             const float dx = (cn * nx + ct * Tx) + cb * Bx;
             const float dy = (cn * ny + ct * Ty) + cb * By;
@@ -840,10 +876,14 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             float4 res;
             if constexpr (BRICK) steps += march_brick<O32, UNION, true, KL>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, tab, pc);
             else steps += march<O32>(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
-            ir = fmaf(wk, res.x, ir);
-            ig = fmaf(wk, res.y, ig);
-            ib = fmaf(wk, res.z, ib);
-            occ = fmaf(wk, res.w, occ);
+            if (S3 && grp == 2) {                // second half: results go to the hand-over scratch
+                if (in_frame || k.compact) st_coherent(&k.sc_cone[(size_t)(c - c_lo) * k.sc_px + oidx], res);
+            } else {
+                ir = fmaf(wk, res.x, ir);
+                ig = fmaf(wk, res.y, ig);
+                ib = fmaf(wk, res.z, ib);
+                occ = fmaf(wk, res.w, occ);
+            }
         }
         dout = sel4(valid, make_float4(ir, ig, ib, 1.0f - occ), dout);
         if (do_spec) {
@@ -869,9 +909,37 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {
             sout = sel4(valid, res, sout);
         }
     }
+    if (S3 && grp != 0) {
+        // split 2 hand-over: leave this half's data, count in; the second wave of
+        // the pair (same block, same wave slot) finishes the cone-order sum
+        const bool px_ok = in_frame || k.compact;
+        if (grp == 1 && px_ok) st_coherent(&k.sc_part[oidx], make_float4(ir, ig, ib, occ));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the device-coherent stores have landed
+        const uint32_t wid = rb * 4u + wave;
+        uint32_t prev = 0;
+        if (lane == 0) prev = atomicAdd(&k.sc_flag[wid], 1u);
+        prev = (uint32_t)__builtin_amdgcn_readfirstlane((int)prev);
+        if (prev == 1u) {                         // the partner has counted in: its data is there
+            float4 acc = make_float4(ir, ig, ib, occ);
+            if (grp == 2 && px_ok) acc = ld_coherent(&k.sc_part[oidx]);
+            const float(*cones)[4] = cone_table(k.nd);
+            for (int c = k.nd_half; c < k.nd; ++c) {
+                const float wk = cones[c][3];
+                float4 res = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (px_ok) res = ld_coherent(&k.sc_cone[(size_t)(c - k.nd_half) * k.sc_px + oidx]);
+                acc.x = fmaf(wk, res.x, acc.x);
+                acc.y = fmaf(wk, res.y, acc.y);
+                acc.z = fmaf(wk, res.z, acc.z);
+                acc.w = fmaf(wk, res.w, acc.w);
+            }
+            dout = sel4(valid, make_float4(acc.x, acc.y, acc.z, 1.0f - acc.w), dout);
+            wr_diff = true;
+            if (lane == 0) k.sc_flag[wid] = 0u;   // ready for the next launch
+        }
+    }
     if (in_frame || k.compact) {
-        if (role != 1) k.diff[oidx] = dout;
-        if (role != 0) k.spec[oidx] = sout;
+        if (wr_diff) k.diff[oidx] = dout;
+        if (wr_spec) k.spec[oidx] = sout;
         if (k.steps_px && in_frame) k.steps_px[pix] = steps;
     }
     if (k.steps_total) {
@@ -906,6 +974,11 @@ int build_step_table(float tau, uint32_t n, uint32_t L, StepRow* rows) {
     return -1;
 }
 
+// launches of at most this many 16x16 blocks split the diffuse cones into two
+// parts (three parts with the specular cone): few blocks per CU, so the tail of
+// the longest waves dominates (a rank of an 8-GPU frame traces 1/8)
+constexpr uint32_t kSplit3MaxBlocks = 1024;   // measured: 3 parts pay off at 1080p / 8 ranks only
+
 hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     const Grid& g = c->grid;
     TraceK k;
@@ -934,23 +1007,51 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.spec_state = c->spec_keys + kSpecSlots;
     k.spec_rows = c->spec_rows;
     k.spec_tabs = (a->variant & 0x100) ? 0 : 1;
-    // diffuse / specular roles in separate workgroups (variant bit 0x200 turns it off);
-    // per-pixel step counts need both roles in one lane, so steps_px keeps one role
+    // cone groups in separate workgroups (variant bits: 0x200 off, 0x400 three parts,
+    // 0x800 two parts; default by launch size); per-pixel step counts need every
+    // cone of a pixel in one lane, so steps_px keeps one part
     k.split = (k.spec_on && k.nd > 0 && !a->steps_px && !(a->variant & 0x200)) ? 1 : 0;
+    k.nd_half = (k.nd + 1) / 2;
+    k.sc_part = k.sc_cone = nullptr; k.sc_flag = nullptr; k.sc_px = 0;
     const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
-    const uint32_t blocks = nlt * 16 * (k.split ? 2u : 1u);
+    uint32_t blocks = nlt * 16;
+    if (k.split && k.nd > 1 && ((a->variant & 0x400) || (!(a->variant & 0x800) && blocks <= kSplit3MaxBlocks))) {
+        // three parts: hand-over scratch [part | cones nd_half..nd-1] per output pixel + flags
+        const size_t npx = k.compact ? (size_t)nlt * VCT_TILE * VCT_TILE : (size_t)a->width * a->height;
+        const size_t fbytes = (size_t)blocks * 4 * sizeof(unsigned);
+        const bool fresh = c->scratch[5].bytes < fbytes;    // flags: zeroed when allocated, then
+        void* fp = nullptr;                                  // reset by the kernel after each hand-over
+        void* sp = nullptr;
+        hipError_t e = scratch_get(c, 5, fbytes, &fp);
+        if (e != hipSuccess) return e;
+        if (fresh && (e = hipMemsetAsync(fp, 0, c->scratch[5].bytes, c->stream)) != hipSuccess) return e;
+        if ((e = scratch_get(c, 6, (size_t)(1 + k.nd - k.nd_half) * npx * sizeof(float4), &sp)) != hipSuccess)
+            return e;
+        k.split = 2;
+        k.sc_flag = (unsigned*)fp;
+        k.sc_part = (float4*)sp;
+        k.sc_cone = k.sc_part + npx;
+        k.sc_px = npx;
+    }
+    blocks *= 1u + (uint32_t)k.split;
     // O32 instantiations need every level below 4 GiB: n <= 512
     const bool o32 = g.n <= 512;
 #define VCT_K4(BRICK, MINW, UNION)                                                                      \
     do {                                                                                               \
-        if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true>), dim3(blocks), dim3(256), 0, c->stream, k); \
+        if (k.split == 2) {                                                                            \
+            if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, true>), dim3(blocks), dim3(256), 0, c->stream, k); \
+            else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, true>), dim3(blocks), dim3(256), 0, c->stream, k);   \
+        } else if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true>), dim3(blocks), dim3(256), 0, c->stream, k); \
         else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false>), dim3(blocks), dim3(256), 0, c->stream, k);    \
     } while (0)
     switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers; 2 bricks without the four-face union
         case 1: VCT_K4(false, 1, true); break;
         case 2: VCT_K4(true, VCT_K4_MIN_WAVES, false); break;
-        case 3: hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false>), dim3(blocks), dim3(256), 0, c->stream, k); break;   // row-major lanes
+        case 3:   // row-major lanes
+            if (k.split == 2) hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false, true>), dim3(blocks), dim3(256), 0, c->stream, k);
+            else hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false>), dim3(blocks), dim3(256), 0, c->stream, k);
+            break;
         default: VCT_K4(true, VCT_K4_MIN_WAVES, true);
     }
 #undef VCT_K4
