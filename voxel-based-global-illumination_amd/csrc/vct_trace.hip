@@ -794,9 +794,12 @@ __device__ __forceinline__ float4 ld_coherent(float4* p) {
 // ===========================================================================
 // the kernel: pixel setup, cone loop, outputs (BRICK = variant 0, else 1)
 // ===========================================================================
-template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true, bool S3 = false>
-__global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {   // S3: the split-2 instantiation
-    __shared__ float4 lds_all[BRICK ? 4 : 1][BRICK ? 2 * kEntrySlots : 1];
+// S3: the split-2 instantiation.  WG1: one wave per workgroup (an 8x8 block): a
+// wave's LDS is released when that wave ends, not when the slowest of four has
+template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true, bool S3 = false,
+          bool WG1 = true>
+__global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
+    __shared__ float4 lds_all[BRICK && !WG1 ? 4 : 1][BRICK ? 2 * kEntrySlots : 1];
     // split: the grid is 2 or 3 parts over the same pixels, dispatched in
     // blockIdx order: split 1 = diffuse cones | specular cone; split 2 = diffuse
     // cones [0, nd_half) | [nd_half, nd) | specular.  The parts are multiples of
@@ -810,7 +813,9 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {   // S3: the s
     const uint32_t b = blockIdx.x - part * nb;
     // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid
     const uint32_t xcd = b & 7, q = nb >> 3, r = nb & 7;
-    const uint32_t rb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    const uint32_t rbw = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    const uint32_t rb = WG1 ? rbw >> 2 : rbw;                 // the 16x16 block
+    const uint32_t wave = WG1 ? (rbw & 3u) : threadIdx.x >> 6;  // its 8x8 quarter
     const uint32_t lt = rb >> 4, sub = rb & 15;
     int c_lo = 0, c_hi = k.nd, grp = 0;        // diffuse cones [c_lo, c_hi); grp 1/2: a half of split 2
     bool do_spec = k.spec_on != 0, wr_diff = true, wr_spec = true;
@@ -823,8 +828,8 @@ __global__ void __launch_bounds__(256, MINW) k4_trace(TraceK k) {   // S3: the s
                if (part == 0) c_hi = k.nd_half; else c_lo = k.nd_half; }
     }
     const bool do_diff = c_hi > c_lo;
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float4* lds = lds_all[BRICK ? wave : 0];
+    const uint32_t lane = threadIdx.x & 63;
+    float4* lds = lds_all[BRICK && !WG1 ? wave : 0];
     PhaseClock pc;
     pc.start();
     // lane -> pixel of the wave's 8x8 block in Morton order (MORTON; else row-major):
@@ -1015,6 +1020,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.sc_part = k.sc_cone = nullptr; k.sc_flag = nullptr; k.sc_px = 0;
     const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
+    const bool wg1 = !(a->variant & 0x1000);    // 0x1000: four waves per workgroup
     uint32_t blocks = nlt * 16;
     if (k.split && k.nd > 1 && ((a->variant & 0x400) || (!(a->variant & 0x800) && blocks <= kSplit3MaxBlocks))) {
         // three parts: hand-over scratch [part | cones nd_half..nd-1] per output pixel + flags
@@ -1035,26 +1041,35 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         k.sc_px = npx;
     }
     blocks *= 1u + (uint32_t)k.split;
+    const uint32_t wgs = wg1 ? 64u : 256u;
+    if (wg1) blocks *= 4u;
     // O32 instantiations need every level below 4 GiB: n <= 512
     const bool o32 = g.n <= 512;
-#define VCT_K4(BRICK, MINW, UNION)                                                                      \
+#define VCT_K4_WG(BRICK, MINW, UNION, WG)                                                               \
     do {                                                                                               \
         if (k.split == 2) {                                                                            \
-            if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, true>), dim3(blocks), dim3(256), 0, c->stream, k); \
-            else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, true>), dim3(blocks), dim3(256), 0, c->stream, k);   \
-        } else if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true>), dim3(blocks), dim3(256), 0, c->stream, k); \
-        else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false>), dim3(blocks), dim3(256), 0, c->stream, k);    \
+            if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, true, WG>), dim3(blocks), dim3(wgs), 0, c->stream, k); \
+            else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, true, WG>), dim3(blocks), dim3(wgs), 0, c->stream, k);   \
+        } else if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, false, WG>), dim3(blocks), dim3(wgs), 0, c->stream, k); \
+        else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, false, WG>), dim3(blocks), dim3(wgs), 0, c->stream, k);    \
+    } while (0)
+#define VCT_K4(BRICK, MINW, UNION)                                                                      \
+    do {                                                                                               \
+        if (wg1) VCT_K4_WG(BRICK, MINW, UNION, true);                                                  \
+        else VCT_K4_WG(BRICK, MINW, UNION, false);                                                     \
     } while (0)
     switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers; 2 bricks without the four-face union
         case 1: VCT_K4(false, 1, true); break;
         case 2: VCT_K4(true, VCT_K4_MIN_WAVES, false); break;
-        case 3:   // row-major lanes
-            if (k.split == 2) hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false, true>), dim3(blocks), dim3(256), 0, c->stream, k);
-            else hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false>), dim3(blocks), dim3(256), 0, c->stream, k);
+        case 3:   // row-major lanes (one wave per workgroup only)
+            if (!wg1) return hipErrorInvalidValue;
+            if (k.split == 2) hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false, true>), dim3(blocks), dim3(wgs), 0, c->stream, k);
+            else hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false>), dim3(blocks), dim3(wgs), 0, c->stream, k);
             break;
         default: VCT_K4(true, VCT_K4_MIN_WAVES, true);
     }
 #undef VCT_K4
+#undef VCT_K4_WG
     return hipGetLastError();
 }
 
