@@ -352,7 +352,8 @@ __device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, f
 // every z step onto the same banks.
 constexpr int kBz = 19;
 constexpr int kBlk = 3 * kBz + 16;              // one face block: 73 slots
-constexpr int kEntrySlots = 4 * kBlk;           // float4 per cache entry (up to 4 face blocks)
+// float4 slots per cache entry: up to 4 face blocks (3 without the four-face union)
+template <bool UNION> constexpr int entry_slots() { return (UNION ? 4 : 3) * kBlk; }
 
 // One wave's LDS hand-off (writes -> other lanes' reads, and reads -> next
 // writes): the asm "memory" clobber keeps the compiler from moving DS ops
@@ -543,8 +544,8 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         bc.b = t;
         bc.flip ^= 1;
     }
-    float4* ldsA = lds + bc.flip * kEntrySlots;
-    float4* ldsB = lds + (bc.flip ^ 1) * kEntrySlots;
+    float4* ldsA = lds + bc.flip * entry_slots<UNION>();
+    float4* ldsB = lds + (bc.flip ^ 1) * entry_slots<UNION>();
     // level A: cached, restaged, or gathered
     const Corner cA = level_corner(l0, qx, qy, qz);
     BrickEntry bA = bc.a;
@@ -799,7 +800,7 @@ __device__ __forceinline__ float4 ld_coherent(float4* p) {
 template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true, bool S3 = false,
           bool WG1 = true>
 __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
-    __shared__ float4 lds_all[BRICK && !WG1 ? 4 : 1][BRICK ? 2 * kEntrySlots : 1];
+    __shared__ float4 lds_all[BRICK && !WG1 ? 4 : 1][BRICK ? 2 * entry_slots<UNION>() : 1];
     // split: the grid is 2 or 3 parts over the same pixels, dispatched in
     // blockIdx order: split 1 = diffuse cones | specular cone; split 2 = diffuse
     // cones [0, nd_half) | [nd_half, nd) | specular.  The parts are multiples of
