@@ -87,7 +87,12 @@ typedef struct vct_trace_args {
     uint32_t tile_rank;    /* trace only 64x64 tiles t with t % tile_world == tile_rank     */
     uint32_t tile_world;   /* 0 or 1: every tile                                            */
     uint32_t tile_compact; /* 1: outputs in rank-compact tile layout [local tile][64*64][4] */
-    uint32_t variant;      /* kernel variant: 0 = default                                  */
+    uint32_t variant;      /* kernel form, 0 = default; all forms give identical results.
+                              low byte: 0 LDS bricks, 1 per-lane gathers, 2 bricks without
+                              the four-face union, 3 row-major lanes; flags: 0x100 no
+                              specular step tables, 0x200 all cones in one workgroup,
+                              0x400 / 0x800 three / two cone parts, 0x1000 four waves
+                              per workgroup                      */
 } vct_trace_args;
 
 /* ---- lifetime ---------------------------------------------------------- */
