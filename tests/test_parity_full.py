@@ -1,0 +1,145 @@
+"""Parity at BASELINE.json's full configuration sizes.
+
+The C oracle finishes these sizes in seconds on the GPU box's host cores, so
+every config is checked against it on the whole frame, not on a scaled-down
+stand-in:
+
+* C2  atrium ("Sponza" stand-in), 128^3, 1280x720, 9 diffuse cones, no specular;
+* C3  atrium, 256^3, 1920x1080, 9 diffuse + 1 specular (the bench / roofline run);
+* C4  atrium, 512^3, 3840x2160, 9 diffuse + 1 specular;
+* C5  courtyard ("San Miguel" stand-in, 1.0 M triangles), 512^3 aniso, 3840x2160,
+      16 diffuse + 1 specular.
+
+Bars (as in test_parity_gpu.py): K1 sums/counts, resolved voxels, K2 radiance and
+the K3 pyramid BIT-EXACT; K4 rel-L2 <= 1e-3 (north_star) over both output buffers,
+and, since the operation order is shared, bit-exact outputs and per-pixel step
+counts.  Size-independent properties checked on the same frames: the kernel's
+cone-step counter equals the sum of its per-pixel counts, a second launch is
+bit-identical, and the multi-GPU screen-tile partition (2/4/8 ranks, traced on
+this one device) reproduces the single-rank frame bit for bit.
+
+G-buffers come from the HIP tile-binned G-buffer pass (row f2), which is
+bit-identical to the brute-force caster (test_parity_gpu.py); they are the
+input here, not the thing checked.
+"""
+import gc
+
+import numpy as np
+import pytest
+
+from helpers import rel_l2
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+TRACE_TOL = 1e-3   # north_star: indirect-irradiance parity within 1e-3 relative L2 (fp32)
+
+CONFIGS = [
+    # id, scene, n, w, h, n_diffuse, specular
+    ("C2", "atrium", 128, 1280, 720, 9, False),
+    ("C3", "atrium", 256, 1920, 1080, 9, True),
+    ("C4", "atrium", 512, 3840, 2160, 9, True),
+    ("C5", "courtyard", 512, 3840, 2160, 16, True),
+]
+
+
+def _pyramid_equal(ctx, O, pyr):
+    """Level-by-level, face-by-face comparison against the oracle's flat pyramid
+    (avoids a second full-size host copy of the GPU pyramid)."""
+    ref = O.pyramid_levels(ctx.n, pyr, ctx.aniso)
+    for l in range(1, ctx.num_levels):
+        _, nf = ctx.level_dims(l)
+        for f in range(nf):
+            if not np.array_equal(ctx.download_level(l, f), ref[l][f]):
+                return (l, f)
+    return None
+
+
+@pytest.mark.parametrize("cid,name,n,w,h,nd,spec", CONFIGS, ids=[c[0] for c in CONFIGS])
+def test_full_config_parity(gpu_ready, oracle_mod, cid, name, n, w, h, nd, spec):
+    import torch
+    from vct import Context, scenes
+    from vct.camera import Camera
+    O = oracle_mod
+    s = scenes.SCENES[name]()
+    v, i, m, k = s.arrays()
+    g0, E = scenes.grid_for_unit_box(n)
+
+    # ---- K1 -> K2 -> K3 vs the oracle pipeline -----------------------------
+    ctx = Context(n, g0, E, aniso=True, n_diffuse=nd, specular=spec)
+    ctx.voxelize(v, i, m, k)
+    ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    ctx.build_mips()
+    sums, counts = O.voxelize(n, g0, E, v, i, m, k)
+    if n <= 256:   # the 64-B accumulator records are 8 GiB at 512^3: compared through the resolved grids there
+        gs, gc_ = ctx.download_accum()
+        assert np.array_equal(gc_, counts), f"{cid}: K1 coverage counts differ"
+        assert np.array_equal(gs, sums), f"{cid}: K1 fixed-point sums differ"
+        del gs, gc_
+    ao, nm = O.resolve(n, sums, counts)
+    del sums, counts
+    gao, gnm = ctx.download_voxels()
+    assert np.array_equal(gao, ao), f"{cid}: resolved albedo/occupancy differs"
+    assert np.array_equal(gnm, nm), f"{cid}: resolved normals differ"
+    del gao, gnm
+    r0 = O.inject(n, ao, nm, scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    del nm
+    assert np.array_equal(ctx.download_level(0), r0), f"{cid}: K2 radiance differs"
+    pyr = O.build_mips(n, r0, True)
+    bad = _pyramid_equal(ctx, O, pyr)
+    assert bad is None, f"{cid}: K3 level/face {bad} differs"
+    occupied = int((ao[..., 3] > 0).sum())
+    del ao
+    gc.collect()
+
+    # ---- K4 on the full frame -----------------------------------------------
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    cam = Camera()
+    gb = tuple(torch.empty((h, w, 4), device=dev) for _ in range(3))
+    ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)
+    d = torch.empty((h, w, 4), device=dev)
+    sp = torch.empty((h, w, 4), device=dev)
+    st = torch.zeros((h, w), dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.trace_device(*gb, w, h, cam.position, d, sp, steps_px=st, cone_steps=cnt)
+    torch.cuda.synchronize()
+    host_gb = [t.cpu().numpy() for t in gb]
+    valid = int((host_gb[0][..., 3] != 0).sum())
+    assert valid > w * h // 4, f"{cid}: G-buffer mostly background ({valid} px)"
+    ref = O.trace(n, g0, E, r0, pyr, *host_gb, cam.position, aniso=True, n_diffuse=nd, specular=spec)
+    del pyr, r0
+    gd, gsp = d.cpu().numpy(), sp.cpu().numpy()
+    both = rel_l2(np.concatenate([gd.ravel(), gsp.ravel()]), np.concatenate([ref["diffuse"].ravel(),
+                                                                            ref["spec"].ravel()]))
+    assert both <= TRACE_TOL, f"{cid}: cone-trace rel L2 {both:.3e}"
+    assert int(cnt.item()) == ref["cone_steps"], f"{cid}: frame cone steps differ"
+    steps = st.cpu().numpy().astype(np.uint32)
+    assert np.array_equal(steps, ref["steps_px"]), f"{cid}: per-pixel step counts differ"
+    assert np.array_equal(gd, ref["diffuse"]) and np.array_equal(gsp, ref["spec"]), f"{cid}: not bit-exact"
+    # size-independent properties
+    assert int(steps.astype(np.uint64).sum()) == int(cnt.item())
+    assert gsp[..., 3].max() <= 1.0 + 1e-6 and gd[..., 3].min() >= -1e-6 and np.isfinite(gd).all()
+    # the bench's launch (no per-pixel counts: cones split over workgroups) equals it too
+    d2, sp2 = torch.full_like(d, -1.0), torch.full_like(sp, -1.0)
+    c2 = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.trace_device(*gb, w, h, cam.position, d2, sp2, cone_steps=c2)
+    torch.cuda.synchronize()
+    assert torch.equal(d2, d) and torch.equal(sp2, sp) and int(c2.item()) == int(cnt.item())
+    # multi-GPU screen tiles: every rank's compact tiles un-permuted == the frame
+    from vct.multi import tiles_for_rank
+    for world in (2, 4, 8):
+        maxt = tiles_for_rank(w, h, 0, world)
+        g = torch.zeros((world, 2, maxt * 4096, 4), device=dev)
+        for r in range(world):
+            ctx.trace_device(*gb, w, h, cam.position, g[r, 0], g[r, 1], tile_rank=r, tile_world=world,
+                             tile_compact=True)
+        fd, fs = torch.zeros_like(d), torch.zeros_like(sp)
+        ctx.untile_planes_device(g, w, h, world, (fd, fs))
+        torch.cuda.synchronize()
+        assert torch.equal(fd, d) and torch.equal(fs, sp), f"{cid}: {world}-rank tiles differ"
+        del g
+    print(f"{cid}: {name} {n}^3 {w}x{h} nd={nd} spec={spec}: occupied={occupied} valid_px={valid} "
+          f"cone_steps={int(cnt.item())} rel_l2={both:.1e}")
+    ctx.close()
+    del gb, d, sp, d2, sp2, st
+    torch.cuda.empty_cache()

@@ -17,7 +17,7 @@ TRACE_TOL = 1e-3   # north_star: indirect-irradiance parity within 1e-3 relative
 
 
 @pytest.mark.parametrize("name,n", [("cornell", 16), ("cornell", 32), ("atrium", 32), ("atrium", 64),
-                                    ("random", 32)])
+                                    ("random", 32), ("courtyard", 64)])
 def test_voxelize_inject_mips_bitexact(gpu_ready, oracle_mod, name, n):
     O = oracle_mod
     ctx, s, (v, i, m, k), (g0, E) = gpu_pipeline(n, name)

@@ -10,6 +10,9 @@ and framebuffer sizes:
   interior (with a closed ceiling every voxel would be in shadow);
 * ``atrium()``: the "Sponza-class" stand-in: an atrium with a long roof
   opening, two colonnades of four columns, two gallery slabs, coloured walls;
+* ``courtyard()``: the "San Miguel-class" stand-in (config C5): an open
+  courtyard of 1.0 M mostly small triangles (tessellated paving and walls,
+  arcades, icosphere tree crowns, tables, hanging foliage);
 * ``random_triangles()``: a triangle soup for voxelization stress / parity.
 
 Geometry is emitted in the reference ``Vertex`` layout (include/stdafx.h:36-42:
@@ -164,7 +167,155 @@ def random_triangles(n_tri: int, seed: int = 7, size: float = 0.3) -> Scene:
     return s
 
 
-SCENES = {"cornell": cornell, "atrium": atrium}
+class ArrayScene(Scene):
+    """A scene built directly as arrays (for million-triangle stand-ins, where the
+    per-triangle list path of :class:`Scene` would be slow).  Triangles are added in
+    batches with the same per-corner vertex rule as :meth:`Scene.tri` (flat face
+    normal, computed in float64, stored as float32)."""
+
+    def __init__(self, name: str):
+        super().__init__(name)
+        self._pos: list = []      # (T,3,3) float64 batches
+        self._mat: list = []      # (T,) int batches
+
+    def tris(self, P: np.ndarray, mat) -> None:
+        P = np.asarray(P, np.float64).reshape(-1, 3, 3)
+        self._pos.append(P)
+        self._mat.append(np.broadcast_to(np.asarray(mat, np.int64), (P.shape[0],)).copy())
+
+    def tri(self, p0, p1, p2, mat: int):
+        self.tris(np.stack([np.asarray(p, np.float64) for p in (p0, p1, p2)])[None], mat)
+
+    def arrays(self):
+        P = np.concatenate(self._pos) if self._pos else np.zeros((0, 3, 3))
+        mat = np.concatenate(self._mat) if self._mat else np.zeros((0,), np.int64)
+        n = np.cross(P[:, 1] - P[:, 0], P[:, 2] - P[:, 0])
+        ln = np.linalg.norm(n, axis=-1, keepdims=True)
+        n = np.where(ln > 0, n / np.where(ln > 0, ln, 1.0), n)
+        T = P.shape[0]
+        verts = np.zeros((T, 3, VERTEX_FLOATS), np.float32)
+        verts[:, :, 0:3] = P
+        verts[:, :, 3:6] = n[:, None, :]
+        return (verts.reshape(-1, VERTEX_FLOATS), np.arange(3 * T, dtype=np.uint32),
+                mat.astype(np.uint32), np.asarray(self.kd, np.float32).reshape(-1, 4))
+
+    @property
+    def n_tri(self):
+        return int(sum(p.shape[0] for p in self._pos))
+
+
+def _grid_quads(xs, zs, y):
+    """Heightfield y(x,z) over the grid xs x zs -> (2*(nx-1)*(nz-1), 3, 3) triangles
+    wound so the face normal points up."""
+    X, Z = np.meshgrid(xs, zs, indexing="xy")
+    Y = y(X, Z)
+    V = np.stack([X, Y, Z], -1)
+    a, b = V[:-1, :-1], V[:-1, 1:]
+    c, d = V[1:, 1:], V[1:, :-1]
+    t1 = np.stack([a, d, c], -2).reshape(-1, 3, 3)
+    t2 = np.stack([a, c, b], -2).reshape(-1, 3, 3)
+    return np.concatenate([t1, t2])
+
+
+def _orient(T: np.ndarray, normal) -> np.ndarray:
+    """Reverse the winding of the triangles whose face normal opposes `normal`."""
+    fn = np.cross(T[:, 1] - T[:, 0], T[:, 2] - T[:, 0])
+    flip = fn @ np.asarray(normal, np.float64) < 0
+    T = T.copy()
+    T[flip] = T[flip][:, ::-1]
+    return T
+
+
+def _icosphere(level: int):
+    """Unit icosphere triangles (20 * 4^level, 3, 3), outward winding."""
+    t = (1 + 5 ** 0.5) / 2
+    v = np.array([(-1, t, 0), (1, t, 0), (-1, -t, 0), (1, -t, 0), (0, -1, t), (0, 1, t), (0, -1, -t), (0, 1, -t),
+                  (t, 0, -1), (t, 0, 1), (-t, 0, -1), (-t, 0, 1)], np.float64)
+    f = np.array([(0, 11, 5), (0, 5, 1), (0, 1, 7), (0, 7, 10), (0, 10, 11), (1, 5, 9), (5, 11, 4), (11, 10, 2),
+                  (10, 7, 6), (7, 1, 8), (3, 9, 4), (3, 4, 2), (3, 2, 6), (3, 6, 8), (3, 8, 9), (4, 9, 5),
+                  (2, 4, 11), (6, 2, 10), (8, 6, 7), (9, 8, 1)])
+    T = v[f]
+    T /= np.linalg.norm(T, axis=-1, keepdims=True)
+    for _ in range(level):
+        a, b, c = T[:, 0], T[:, 1], T[:, 2]
+        ab, bc, ca = (a + b) / 2, (b + c) / 2, (c + a) / 2
+        ab, bc, ca = (x / np.linalg.norm(x, axis=-1, keepdims=True) for x in (ab, bc, ca))
+        T = np.concatenate([np.stack(q, 1) for q in ((a, ab, ca), (ab, b, bc), (ca, bc, c), (ab, bc, ca))])
+    return T
+
+
+def _box_tris(lo, hi):
+    s = Scene("tmp")
+    s.box(lo, hi, 0)
+    return np.asarray(s.verts, np.float64)[:, :3].reshape(-1, 3, 3)
+
+
+def courtyard(seed: int = 11) -> Scene:
+    """"San Miguel-class" stand-in (BASELINE config C5): an open courtyard with
+    ~1.1 M triangles, most of them small: a finely tessellated undulating paving
+    (the bulk of the count), arcaded walls, tessellated tree crowns on trunks,
+    tables, and a hanging-foliage triangle soup along the upper arcade."""
+    rng = np.random.default_rng(seed)
+    s = ArrayScene("courtyard")
+    paving = s.material((0.60, 0.52, 0.42))
+    plaster = s.material((0.78, 0.70, 0.55))
+    terracotta = s.material((0.65, 0.30, 0.18))
+    bark = s.material((0.35, 0.25, 0.15))
+    leaves = s.material((0.18, 0.42, 0.12))
+    wood = s.material((0.50, 0.33, 0.20))
+    # paving: 600 x 600 quads, gentle undulation (720 K triangles)
+    xs = np.linspace(-1.0, 1.0, 601)
+    s.tris(_grid_quads(xs, xs, lambda X, Z: -0.985 + 0.015 * np.sin(7 * X) * np.cos(5 * Z)), paving)
+    # walls (back, left, right), tessellated 120 x 120 each (86 K triangles)
+    ws = np.linspace(-1.0, 1.0, 121)
+    wall = _grid_quads(ws, ws, lambda X, Z: np.zeros_like(X))    # (a, 0, b) grid
+    a, b = wall[..., 0], wall[..., 2]
+    one = np.ones_like(a)
+    s.tris(_orient(np.stack([a, b, -one], -1), (0, 0, 1)), plaster)       # back  z = -1, normal +z
+    s.tris(_orient(np.stack([-one, a, b], -1), (1, 0, 0)), terracotta)    # left  x = -1, normal +x
+    s.tris(_orient(np.stack([one, a, b], -1), (-1, 0, 0)), terracotta)    # right x = +1, normal -x
+    # arcade: piers and an upper gallery slab along the three walls
+    for k in range(7):
+        z = -0.9 + k * 0.3
+        s.tris(_box_tris((-0.86, -1.0, z - 0.04), (-0.78, 0.1, z + 0.04)), plaster)
+        s.tris(_box_tris((0.78, -1.0, z - 0.04), (0.86, 0.1, z + 0.04)), plaster)
+    for k in range(6):
+        x = -0.75 + k * 0.3
+        s.tris(_box_tris((x - 0.04, -1.0, -0.86), (x + 0.04, 0.1, -0.78)), plaster)
+    s.tris(_box_tris((-1.0, 0.1, -1.0), (-0.75, 0.18, 0.95)), plaster)
+    s.tris(_box_tris((0.75, 0.1, -1.0), (1.0, 0.18, 0.95)), plaster)
+    s.tris(_box_tris((-0.75, 0.1, -1.0), (0.75, 0.18, -0.75)), plaster)
+    # trees: trunks + icosphere crowns (level 4: 5120 triangles each)
+    crown = _icosphere(4)
+    for (tx, tz, r) in ((-0.4, -0.3, 0.22), (0.35, -0.45, 0.25), (0.05, 0.3, 0.18), (-0.45, 0.45, 0.16),
+                        (0.5, 0.35, 0.2)):
+        top = -0.35 + r
+        s.tris(_box_tris((tx - 0.025, -1.0, tz - 0.025), (tx + 0.025, top - r * 0.5, tz + 0.025)), bark)
+        for j in range(3):
+            off = rng.uniform(-0.5, 0.5, 3) * r
+            s.tris(crown * (r * rng.uniform(0.6, 0.9)) + np.array([tx, top, tz]) + off, leaves)
+    # tables with tops and legs (dining area)
+    for k in range(24):
+        cx, cz = rng.uniform(-0.65, 0.65), rng.uniform(-0.65, 0.75)
+        s.tris(_box_tris((cx - 0.07, -0.78, cz - 0.07), (cx + 0.07, -0.76, cz + 0.07)), wood)
+        for dx in (-0.05, 0.05):
+            for dz in (-0.05, 0.05):
+                s.tris(_box_tris((cx + dx - 0.006, -1.0, cz + dz - 0.006), (cx + dx + 0.006, -0.78, cz + dz + 0.006)),
+                       wood)
+    # hanging foliage on the gallery edge: 120 K small triangles
+    nf = 120_000
+    side = rng.integers(0, 3, nf)
+    u = rng.uniform(-0.95, 0.95, nf)
+    yy = rng.uniform(-0.35, 0.1, nf)
+    c = np.where(side[:, None] == 0, np.stack([np.full(nf, -0.74), yy, u], -1),
+                 np.where(side[:, None] == 1, np.stack([np.full(nf, 0.74), yy, u], -1),
+                          np.stack([u * 0.78, yy, np.full(nf, -0.74)], -1)))
+    c += rng.uniform(-0.03, 0.03, c.shape)
+    s.tris(c[:, None, :] + rng.uniform(-0.012, 0.012, (nf, 3, 3)), leaves)
+    return s
+
+
+SCENES = {"cornell": cornell, "atrium": atrium, "courtyard": courtyard}
 
 
 # ---------------------------------------------------------------------------
