@@ -94,13 +94,24 @@ def cpu_baseline(ctx, n, g0, E, gb_host, eye, n_diffuse, spec, steps_px_gpu, tar
     dt = time.perf_counter() - t0
     rows = list(range(0, h, row_step))
     match = bool(np.array_equal(res["steps_px"][rows], steps_px_gpu[rows]))
+    steps, reps = res["cone_steps"], 1
+    if row_step == 1 and dt < 0.5 * target_s:
+        # the whole frame takes less than the target: time repeated whole frames instead
+        reps = min(50, max(1, int(math.ceil(target_s / max(dt, 1e-3)))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            O.trace(n, g0, E, r0, pyr, pos, nrm, alb, eye, aniso=True, n_diffuse=n_diffuse, specular=spec,
+                    row_step=1, threads=cores)
+        dt = time.perf_counter() - t0
+        steps *= reps
+    sample = (f"whole frame x {reps} ({res['cone_steps']} cone steps each, {dt:.1f} s)" if row_step == 1 else
+              f"rows y % {row_step} == 0 ({len(rows)} of {h} rows, {res['cone_steps']} cone steps, {dt:.1f} s)")
     return {
-        "value": res["cone_steps"] / dt / 1e6,
+        "value": steps / dt / 1e6,
         "unit": "Mcone-steps/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"rows y % {row_step} == 0 ({len(rows)} of {h} rows, {res['cone_steps']} cone steps, "
-                  f"{dt:.1f} s); C oracle -O3 x86-64-v3 OpenMP",
+        "sample": sample + "; C oracle -O3 x86-64-v3 OpenMP",
         "steps_match_gpu": match,
     }
 
@@ -170,7 +181,7 @@ def main():
     eye = [float(x) for x in cam.position]
     if args.gbuffer == "scene":
         gb = tuple(torch.empty((h, w, 4), dtype=torch.float32, device=dev) for _ in range(3))
-        ctx.gbuffer_raycast_device(cam, w, h, scenes.ROUGHNESS, *gb)
+        ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)   # row f2, == the ray caster
     else:
         ao, nm = ctx.download_voxels()
         host = scenes.gbuffer_rand(ao, nm, g0, E, w, h, seed=42)
@@ -260,6 +271,8 @@ def main():
             "k2_inject_ms": round(k2_ms, 3),
             "k3_mips_ms": round(k3_ms, 3),
             "grid_bcast_ms": round(bcast_ms, 3),
+            # a frame whose light changes: inject + mips + trace (+ the broadcast at N > 1)
+            "frame_relight_ms": round(k2_ms + bcast_ms + k3_ms + ms_per_step, 3),
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),

@@ -43,7 +43,7 @@ def main():
     cam = Camera()
     if a.gbuffer == "scene":
         gb = [torch.empty((a.h, a.w, 4), device=dev) for _ in range(3)]
-        ctx.gbuffer_raycast_device(cam, a.w, a.h, scenes.ROUGHNESS, *gb)
+        ctx.gbuffer_raster_device(cam, a.w, a.h, scenes.ROUGHNESS, *gb)
     else:
         ao, nm = ctx.download_voxels()
         gb = [torch.from_numpy(x).to(dev) for x in scenes.gbuffer_rand(ao, nm, g0, E, a.w, a.h)]

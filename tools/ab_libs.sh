@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 for r in $(seq 1 ${3:-3}); do
   for L in "$1" "$2"; do
-    VCT_LIB=$L timeout -k 10 200 python tools/ab.py --variants 0 --rounds 5 > gpurun_out/ab_lib.json 2>&1 || exit 1
+    VCT_LIB=$L timeout -k 10 200 python tools/ab.py --variants 0 --rounds 5 ${AB_ARGS:-} > gpurun_out/ab_lib.json 2>&1 || exit 1
     echo "$L $(grep -m1 median gpurun_out/ab_lib.json)"
   done
 done

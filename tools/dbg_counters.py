@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--gbuffer", default="scene")
+    ap.add_argument("--scene", default="atrium")
     ap.add_argument("--clk", action="store_true", help="phase clocks (make clk) instead of path counters")
     ap.add_argument("--variants", default="0")
     a = ap.parse_args()
@@ -37,7 +38,7 @@ def main():
     g0, E = scenes.grid_for_unit_box(a.n)
     ctx = Context(a.n, g0, E)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-    s = scenes.atrium()
+    s = scenes.SCENES[a.scene]()
     ctx.voxelize(*s.arrays())
     ctx.inject_directional(scenes.LIGHT_DIR)
     ctx.build_mips()
@@ -45,7 +46,7 @@ def main():
     cam = Camera()
     if a.gbuffer == "scene":
         gb = [torch.empty((a.h, a.w, 4), device=dev) for _ in range(3)]
-        ctx.gbuffer_raycast_device(cam, a.w, a.h, scenes.ROUGHNESS, *gb)
+        ctx.gbuffer_raster_device(cam, a.w, a.h, scenes.ROUGHNESS, *gb)
     else:
         ao, nm = ctx.download_voxels()
         gb = [torch.from_numpy(x).to(dev) for x in scenes.gbuffer_rand(ao, nm, g0, E, a.w, a.h)]

@@ -40,7 +40,7 @@ def main():
     dev = torch.device("cuda")
     cam = Camera()
     gb = [torch.empty((a.h, a.w, 4), device=dev) for _ in range(3)]
-    ctx.gbuffer_raycast_device(cam, a.w, a.h, scenes.ROUGHNESS, *gb)
+    ctx.gbuffer_raster_device(cam, a.w, a.h, scenes.ROUGHNESS, *gb)
 
     def timed(fn):
         ts = []
