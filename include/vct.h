@@ -117,6 +117,13 @@ vct_status  vct_synchronize(vct_ctx* ctx);
 vct_status vct_voxelize(vct_ctx* ctx, const void* verts, uint32_t vertex_stride, uint32_t n_verts,
                         const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_material,
                         const float* material_kd4, uint32_t n_materials);
+/* Same, on geometry already resident on the device (the reference's meshes live
+ * in GL buffers after Mesh::setupMesh, mesh.cpp:31-64): every array is a device
+ * pointer (verts 4-byte, material_kd4 16-byte aligned).  Returns after K1 has
+ * finished (it reads back one candidate count to size its grid). */
+vct_status vct_voxelize_device(vct_ctx* ctx, const void* verts, uint32_t vertex_stride, uint32_t n_verts,
+                               const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_material,
+                               const float* material_kd4, uint32_t n_materials);
 
 /* ---- K2 direct-light injection (A.3) ----------------------------------- */
 vct_status vct_inject_directional(vct_ctx* ctx, const float dir_to_light[3], const float color[3]);

@@ -411,6 +411,41 @@ def test_voxelize_reproducible_and_rerun(gpu_ready):
     ctx.close()
 
 
+def test_voxelize_sequence_resets_sparsely(gpu_ready, oracle_mod):
+    """K1 clears only what the previous call set (records, voxels, bits): a sequence
+    of different scenes on one context, and the device-resident entry point, give
+    exactly the oracle's result for the last scene; K2 and the mips follow it."""
+    import torch
+    from vct import Context, scenes
+    from helpers import scene_arrays
+    n = 64
+    g0, E = scenes.grid_for_unit_box(n)
+    ctx = Context(n, g0, E)
+    seq = ["atrium", "cornell", "random", "atrium", "cornell"]
+    for j, name in enumerate(seq):
+        _, (v, i, m, k) = scene_arrays(name)
+        if j % 2:
+            dev = torch.device("cuda")
+            ctx.voxelize_device(torch.from_numpy(v).to(dev), torch.from_numpy(i.astype(np.int32)).to(dev),
+                                torch.from_numpy(m.astype(np.int32)).to(dev), torch.from_numpy(k).to(dev))
+        else:
+            ctx.voxelize(v, i, m, k)
+        ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+        ctx.build_mips()
+        ref = oracle_mod.pipeline(n, g0, E, v, i, m, k, scenes.LIGHT_DIR)
+        sums, counts = ctx.download_accum()
+        assert np.array_equal(counts, ref["counts"]) and np.array_equal(sums, ref["sums"]), name
+        ao, nm = ctx.download_voxels()
+        assert np.array_equal(ao, ref["albedo_occ"]) and np.array_equal(nm, ref["normal"]), name
+        assert np.array_equal(ctx.download_level(0), ref["r0"]), name
+        assert np.array_equal(gpu_pyramid_flat(ctx), ref["pyr"]), name
+    # an empty mesh clears the grid
+    ctx.voxelize(np.zeros((0, 14), np.float32), np.zeros(0, np.uint32))
+    ao, nm = ctx.download_voxels()
+    assert not ao.any() and not nm.any()
+    ctx.close()
+
+
 @pytest.mark.parametrize("name,n", [("cornell", 32), ("atrium", 64)])
 def test_composite_matches_oracle(gpu_ready, oracle_mod, name, n):
     """Row f3: composite + present on the GPU equals the oracle: linear output

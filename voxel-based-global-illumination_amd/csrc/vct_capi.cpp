@@ -138,6 +138,11 @@ vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
     if (e == hipSuccess) e = hipMalloc(&g.normal, nv * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&g.occ_bits, (nv / 64) * 8);
     if (e == hipSuccess) e = hipMalloc((void**)&g.accum, nv * 64);
+    // K1's sparse-reset invariant: accumulators, voxels and bits start at zero
+    if (e == hipSuccess) e = hipMemset(g.accum, 0, nv * 64);
+    if (e == hipSuccess) e = hipMemset(g.albedo_occ, 0, nv * sizeof(float4));
+    if (e == hipSuccess) e = hipMemset(g.normal, 0, nv * sizeof(float4));
+    if (e == hipSuccess) e = hipMemset(g.occ_bits, 0, (nv / 64) * 8);
     if (e == hipSuccess) {
         StepRow rows[kMaxStepRows];
         const float tau_d = cfg->n_diffuse == 16 ? VCT_TAN20 : VCT_TAN30;
@@ -168,6 +173,7 @@ void vct_destroy(vct_ctx* c) {
     if (g.normal) (void)hipFree(g.normal);
     if (g.occ_bits) (void)hipFree(g.occ_bits);
     if (g.accum) (void)hipFree(g.accum);
+    if (c->k1_err) (void)hipFree(c->k1_err);
     if (c->mesh.tri) (void)hipFree(c->mesh.tri);
     if (c->step_tab) (void)hipFree(c->step_tab);
     if (c->spec_keys) (void)hipFree(c->spec_keys);
@@ -197,15 +203,45 @@ vct_status vct_synchronize(vct_ctx* c) {
     return VCT_OK;
 }
 
-vct_status vct_voxelize(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
-                        const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
-                        const float* kd4, uint32_t n_mat) {
+static vct_status voxelize_args(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_idx, const uint32_t* idx,
+                                const float* kd4, uint32_t n_mat) {
     if (!c) return VCT_EINVAL;
     if (n_idx % 3 != 0) return fail(c, VCT_EINVAL, "n_idx must be a multiple of 3");
     if (n_idx > 0 && (!verts || !idx)) return fail(c, VCT_EINVAL, "null vertex or index array");
-    if (stride < 12) return fail(c, VCT_EINVAL, "vertex_stride < 12");
+    if (stride < 12 || stride % 4 != 0) return fail(c, VCT_EINVAL, "vertex_stride < 12 or not a multiple of 4");
     if (kd4 && n_mat == 0) return fail(c, VCT_EINVAL, "material_kd4 with n_materials == 0");
-    vct_status st = use_device(c);
+    return use_device(c);
+}
+
+// K1 on device-resident geometry; `derr` (device int) receives the index-range flag
+static vct_status voxelize_dev(vct_ctx* c, const void* dv, uint32_t stride, uint32_t n_verts, const uint32_t* di,
+                               uint32_t n_tri, const uint32_t* dm, const float4* dk, uint32_t n_mat, int* derr) {
+    Mesh& m = c->mesh;
+    const size_t tri_bytes = (size_t)(n_tri ? n_tri : 1) * 4 * sizeof(float4);
+    if (m.cap < tri_bytes) {
+        VCT_HIP(hipStreamSynchronize(c->stream), "sync");
+        if (m.tri) (void)hipFree(m.tri);
+        m.tri = nullptr;
+        m.cap = 0;
+        VCT_HIP(hipMalloc(&m.tri, tri_bytes), "hipMalloc mesh");
+        m.cap = tri_bytes;
+    }
+    m.n_tri = n_tri;
+    VCT_HIP(hipMemsetAsync(derr, 0, 4, c->stream), "memset err");
+    VCT_HIP(launch_voxelize(c, dv, stride, n_verts, di, n_tri, dm, dk, n_mat, derr), "voxelize");
+    int herr = 0;
+    VCT_HIP(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, c->stream), "download err");
+    VCT_HIP(hipStreamSynchronize(c->stream), "voxelize sync");
+    c->grid.voxelized = true;
+    c->grid.injected = c->grid.mipped = false;
+    if (herr) return fail(c, VCT_EINVAL, "vertex or material index out of range");
+    return VCT_OK;
+}
+
+vct_status vct_voxelize(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                        const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
+                        const float* kd4, uint32_t n_mat) {
+    vct_status st = voxelize_args(c, verts, stride, n_idx, idx, kd4, n_mat);
     if (st != VCT_OK) return st;
     const uint32_t n_tri = n_idx / 3;
     // host -> device staging (the reference keeps CPU copies of vertices / indices
@@ -221,28 +257,19 @@ vct_status vct_voxelize(vct_ctx* c, const void* verts, uint32_t stride, uint32_t
     if (n_idx) VCT_HIP(hipMemcpyAsync(di.p, idx, (size_t)n_idx * 4, hipMemcpyHostToDevice, c->stream), "upload idx");
     if (dm.p) VCT_HIP(hipMemcpyAsync(dm.p, tri_mat, (size_t)n_tri * 4, hipMemcpyHostToDevice, c->stream), "upload mat");
     if (dk.p) VCT_HIP(hipMemcpyAsync(dk.p, kd4, (size_t)n_mat * 16, hipMemcpyHostToDevice, c->stream), "upload kd");
-    VCT_HIP(hipMemsetAsync(derr.p, 0, 4, c->stream), "memset err");
-    Mesh& m = c->mesh;
-    const size_t tri_bytes = (size_t)(n_tri ? n_tri : 1) * 4 * sizeof(float4);
-    if (m.cap < tri_bytes) {
-        VCT_HIP(hipStreamSynchronize(c->stream), "sync");
-        if (m.tri) (void)hipFree(m.tri);
-        m.tri = nullptr;
-        m.cap = 0;
-        VCT_HIP(hipMalloc(&m.tri, tri_bytes), "hipMalloc mesh");
-        m.cap = tri_bytes;
-    }
-    m.n_tri = n_tri;
-    VCT_HIP(launch_voxelize(c, dv.p, stride, n_verts, (const uint32_t*)di.p, n_tri,
-                            (const uint32_t*)dm.p, (const float4*)dk.p, n_mat, (int*)derr.p),
-            "voxelize");
-    int herr = 0;
-    VCT_HIP(hipMemcpyAsync(&herr, derr.p, 4, hipMemcpyDeviceToHost, c->stream), "download err");
-    VCT_HIP(hipStreamSynchronize(c->stream), "voxelize sync");
-    c->grid.voxelized = true;
-    c->grid.injected = c->grid.mipped = false;
-    if (herr) return fail(c, VCT_EINVAL, "vertex or material index out of range");
-    return VCT_OK;
+    return voxelize_dev(c, dv.p, stride, n_verts, (const uint32_t*)di.p, n_tri, (const uint32_t*)dm.p,
+                        (const float4*)dk.p, n_mat, (int*)derr.p);
+}
+
+vct_status vct_voxelize_device(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                               const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
+                               const float* kd4, uint32_t n_mat) {
+    vct_status st = voxelize_args(c, verts, stride, n_idx, idx, kd4, n_mat);
+    if (st != VCT_OK) return st;
+    if ((kd4 && ((uintptr_t)kd4 & 15)) || ((uintptr_t)verts & 3))
+        return fail(c, VCT_EINVAL, "material_kd4 must be 16-byte and verts 4-byte aligned");
+    if (!c->k1_err) VCT_HIP(hipMalloc((void**)&c->k1_err, 4), "hipMalloc err");
+    return voxelize_dev(c, verts, stride, n_verts, idx, n_idx / 3, tri_mat, (const float4*)kd4, n_mat, c->k1_err);
 }
 
 vct_status vct_inject_directional(vct_ctx* c, const float dir[3], const float color[3]) {

@@ -53,6 +53,7 @@ struct vct_ctx {
     vct::StepRow* step_tab = nullptr;   // [kMaxStepRows] diffuse-cone step table (device)
     unsigned* spec_keys = nullptr;      // [2 * kSpecSlots]: specular table keys (~0u free), then states
     vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)
+    int* k1_err = nullptr;              // device flag of vct_voxelize_device (index out of range)
     std::string err;
 };
 

@@ -11,7 +11,11 @@
 // accumulated with 64-bit integer atomics on 16.16 fixed-point values, so the
 // result is independent of atomic arrival order: bit-exact and reproducible.
 // Per-voxel accumulators are 64-byte records [albedo rgb, normal xyz, count,
-// pad] so a voxel's seven atomics land in one half cache line.
+// pad] so a voxel's seven atomics land in one half cache line.  The first hit
+// of a voxel sets its occupancy bit; resolve and the next call's reset touch
+// only the voxels whose bit is set, so a voxelization costs O(candidates +
+// occupied voxels) plus a 2 MiB bitmask scan at 256^3, not a 1 GiB stream
+// (ctx invariant: records, voxels and bits are zero where no bit is set).
 #include <algorithm>
 #include <cstdlib>
 
@@ -220,7 +224,8 @@ __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__
                                                      const TriFix* __restrict__ fixr,
                                                      const unsigned long long* __restrict__ offs,
                                                      uint32_t n_tri, const unsigned long long* __restrict__ total_p,
-                                                     int n, long long* __restrict__ accum) {
+                                                     int n, long long* __restrict__ accum,
+                                                     unsigned long long* __restrict__ occ_bits) {
     const unsigned long long total = *total_p;
     const unsigned long long c0 = ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x) * kCandPerThread;
     if (c0 >= total) return;
@@ -254,32 +259,47 @@ __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__
         const TriFix& f = fixr[t];
 #pragma unroll
         for (int i = 0; i < 6; ++i) atomicAdd(a + i, (unsigned long long)f.fix[i]);
-        atomicAdd(a + 6, 1ull);
+        if (atomicAdd(a + 6, 1ull) == 0ull) atomicOr(occ_bits + (v >> 6), 1ull << (v & 63));   // first hit
     }
 }
 
-// K1 resolve: accumulators -> albedo/occupancy, normal, occupancy bitmask
+// Sparse reset before a voxelization: the records, voxels and bits the previous
+// one set (everything else is zero by the ctx invariant), so K1 never streams the
+// n^3 x 64-B accumulators.  One wave per bitmask word.
+__global__ void __launch_bounds__(256) k1_clear(unsigned long long* __restrict__ occ_bits, size_t nv,
+                                                long long* __restrict__ accum, float4* __restrict__ albedo_occ,
+                                                float4* __restrict__ normal) {
+    const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nv) return;
+    const unsigned long long w = occ_bits[v >> 6];
+    if (w == 0ull) return;                       // wave-uniform
+    if ((w >> (v & 63)) & 1ull) {
+        longlong2* a = (longlong2*)(accum + 8 * v);
+        const longlong2 z = make_longlong2(0, 0);
+        a[0] = z; a[1] = z; a[2] = z; a[3] = z;
+        albedo_occ[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        normal[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    if ((threadIdx.x & 63) == 0) occ_bits[v >> 6] = 0ull;   // after every lane has read it (one wave)
+}
+
+// K1 resolve: accumulators -> albedo/occupancy, normal of the voxels K1 hit
+// (their bits; the other voxels stay zero)
 __global__ void __launch_bounds__(256) k1_resolve(const long long* __restrict__ accum, size_t nv,
                                                   float4* __restrict__ albedo_occ,
                                                   float4* __restrict__ normal,
-                                                  unsigned long long* __restrict__ occ_bits) {
+                                                  const unsigned long long* __restrict__ occ_bits) {
     size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool in = v < nv;
-    long long s[7] = {0, 0, 0, 0, 0, 0, 0};
-    if (in) {
+    if (v >= nv) return;
+    const unsigned long long w = occ_bits[v >> 6];
+    if (!((w >> (v & 63)) & 1ull)) return;
+    long long s[7];
+    {
         const longlong2* a = (const longlong2*)(accum + 8 * v);
         longlong2 p0 = a[0], p1 = a[1], p2 = a[2], p3 = a[3];
         s[0] = p0.x; s[1] = p0.y; s[2] = p1.x; s[3] = p1.y; s[4] = p2.x; s[5] = p2.y; s[6] = p3.x;
     }
     const unsigned long long cnt = (unsigned long long)s[6];
-    unsigned long long mask = __ballot(in && cnt > 0);
-    if (in && (threadIdx.x & 63) == 0) occ_bits[v >> 6] = mask;
-    if (!in) return;
-    if (cnt == 0) {
-        albedo_occ[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        normal[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        return;
-    }
     double den = (double)cnt * VCT_FIXED_ONE_D;
     float4 ao = make_float4((float)((double)s[0] / den), (float)((double)s[1] / den),
                             (float)((double)s[2] / den), 1.0f);
@@ -566,7 +586,9 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
     unsigned long long* tiles = (unsigned long long*)(base + off_tiles);
     unsigned long long* total = (unsigned long long*)(base + off_total);
 
-    if ((e = hipMemsetAsync(g.accum, 0, nv * 64, s)) != hipSuccess) return e;
+    // sparse reset of the previous voxelization (accum / voxels / bits are zero elsewhere)
+    hipLaunchKernelGGL(k1_clear, dim3((uint32_t)((nv + 255) / 256)), dim3(256), 0, s, g.occ_bits, nv, g.accum,
+                       g.albedo_occ, g.normal);
     if ((e = hipMemsetAsync(total, 0, 8, s)) != hipSuccess) return e;
     if (n_tri > 0) {
         hipLaunchKernelGGL(k1_tri_setup, dim3((n_tri + 255) / 256), dim3(256), 0, s,
@@ -586,7 +608,7 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
             unsigned long long blocks = (threads + 255) / 256;
             if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
             hipLaunchKernelGGL(k1_candidates, dim3((uint32_t)blocks), dim3(256), 0, s, geom, fix, offs,
-                               n_tri, total, (int)g.n, g.accum);
+                               n_tri, total, (int)g.n, g.accum, g.occ_bits);
         }
     }
     hipLaunchKernelGGL(k1_resolve, dim3((uint32_t)((nv + 255) / 256)), dim3(256), 0, s, g.accum, nv,

@@ -129,6 +129,17 @@ class Context:
                                    0 if kd is None else kd.shape[0])
         self._check(st, "voxelize")
 
+    def voxelize_device(self, verts, idx, tri_material=None, kd4=None):
+        """K1 on device-resident torch tensors: verts [V, F] float32 (F >= 3, the
+        56-byte Vertex is F = 14), idx [3T] int32/uint32, tri_material [T] int32,
+        kd4 [M, 4] float32."""
+        assert verts.dim() == 2 and verts.shape[1] >= 3 and verts.is_contiguous()
+        ptr = lambda t: None if t is None else t.data_ptr()
+        nm = 0 if kd4 is None else kd4.shape[0]
+        st = self.lib.vct_voxelize_device(self.h, ptr(verts), verts.shape[1] * 4, verts.shape[0], ptr(idx),
+                                          idx.numel(), ptr(tri_material), ptr(kd4), nm)
+        self._check(st, "voxelize_device")
+
     def inject_directional(self, dir_to_light, color=(1.0, 1.0, 1.0)):
         l = (C.c_float * 3)(*[float(x) for x in dir_to_light])
         c = (C.c_float * 3)(*[float(x) for x in color])
