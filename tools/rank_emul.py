@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
-    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--variant", type=lambda x: int(x, 0), default=0)
+    ap.add_argument("--scene", default="atrium")
     a = ap.parse_args()
     import torch
     from vct import Context, scenes

@@ -42,6 +42,12 @@
 __device__ unsigned long long vct_dbg_ctr[32];
 __device__ unsigned long long vct_dbg_time[8];
 #endif
+#ifdef VCT_DEBUG_CLOCK
+// per-wave (start, end) of the real-time counter (100 MHz, chip-wide), indexed by
+// blockIdx * waves-per-block + wave; tools/wave_sched.py replays schedules from it
+constexpr int kDbgWaves = 1 << 18;
+__device__ unsigned long long vct_dbg_wave[kDbgWaves][3];   // start, end, HW_ID | XCC_ID << 32
+#endif
 #ifdef VCT_DEBUG_COUNTERS
 #define VCT_DBG(i) do { if ((threadIdx.x & 63) == 0) atomicAdd(&vct_dbg_ctr[i], 1ull); } while (0)
 #else
@@ -127,6 +133,8 @@ struct TraceK {
     int split;                   // 0: one workgroup per 16x16 block traces every cone; 1: two (diffuse | specular);
                                  // 2: three (diffuse cones [0, nd_half) | [nd_half, nd) | specular)
     int nd_half;
+    int spec_first;              // split 1: the specular part is dispatched first (variant bit 0x2000)
+    int xcd_g;                   // units per XCD chunk of the workgroup map (0 = one contiguous run per XCD)
     float4* sc_part;             // split 2: [px] diffuse sum after cones [0, nd_half)  (per output index)
     float4* sc_cone;             // split 2: [cone - nd_half][px] results of cones [nd_half, nd)
     size_t sc_px;                // pixels per scratch plane
@@ -812,16 +820,32 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     const uint32_t nb = S3 ? gridDim.x / 3u : (k.split ? gridDim.x >> 1 : gridDim.x);
     const uint32_t part = blockIdx.x >= nb ? (blockIdx.x >= 2u * nb ? 2u : 1u) : 0u;
     const uint32_t b = blockIdx.x - part * nb;
-    // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid
-    const uint32_t xcd = b & 7, q = nb >> 3, r = nb & 7;
-    const uint32_t rbw = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid.
+    // The hardware hands workgroup b to XCD b & 7.  Units (waves with WG1, else
+    // 16x16 blocks) are dealt to the XCDs in chunks of G consecutive units (the
+    // pixels of a chunk share that XCD's L2), chunk c to XCD c & 7, so every XCD
+    // gets a screen-wide sample of the frame: cost varies strongly across the
+    // image (the atrium's middle rows cost ~2x its top and bottom rows), and
+    // with one contiguous run of tiles per XCD the slowest XCD set the launch.
+    // Units past the last full round of 8 chunks go round-robin.  k.xcd_g = 0:
+    // one contiguous run per XCD (the earlier map, kept for A/B).
+    const uint32_t xcd = b & 7;
+    uint32_t rbw;
+    if (k.xcd_g == 0) {
+        const uint32_t q = nb >> 3, r = nb & 7;
+        rbw = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    } else {
+        const uint32_t G = (uint32_t)k.xcd_g, full = (nb / (8u * G)) * (8u * G);
+        const uint32_t kk = b >> 3;
+        rbw = b < full ? G * (xcd + 8u * (kk / G)) + kk % G : b;
+    }
     const uint32_t rb = WG1 ? rbw >> 2 : rbw;                 // the 16x16 block
     const uint32_t wave = WG1 ? (rbw & 3u) : threadIdx.x >> 6;  // its 8x8 quarter
     const uint32_t lt = rb >> 4, sub = rb & 15;
     int c_lo = 0, c_hi = k.nd, grp = 0;        // diffuse cones [c_lo, c_hi); grp 1/2: a half of split 2
     bool do_spec = k.spec_on != 0, wr_diff = true, wr_spec = true;
     if (k.split == 1) {
-        if (part == 0) { do_spec = false; wr_spec = false; }
+        if ((part == 0) != (k.spec_first != 0)) { do_spec = false; wr_spec = false; }
         else { c_hi = 0; wr_diff = false; }
     } else if (S3) {
         if (part == 2) { c_hi = 0; wr_diff = false; }
@@ -833,6 +857,9 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     float4* lds = lds_all[BRICK && !WG1 ? wave : 0];
     PhaseClock pc;
     pc.start();
+#ifdef VCT_DEBUG_CLOCK
+    const unsigned long long wave_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // lane -> pixel of the wave's 8x8 block in Morton order (MORTON; else row-major):
     // the lanes of each ds_read_b128 / load group are then a compact 2x2 / 4x4 pixel block
     const uint32_t mx = MORTON ? (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4) : lane & 7;
@@ -957,6 +984,18 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
         if (lane == 0 && wt) atomicAdd(k.texels_total, (unsigned long long)wt);
     }
     pc.flush();
+#ifdef VCT_DEBUG_CLOCK
+    {
+        const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        if (lane == 0 && wid < (uint32_t)kDbgWaves) {
+            vct_dbg_wave[wid][0] = wave_t0;
+            vct_dbg_wave[wid][1] = __builtin_amdgcn_s_memrealtime();
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);      // HW_REG_HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);    // HW_REG_XCC_ID
+            vct_dbg_wave[wid][2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        }
+    }
+#endif
 }
 
 }  // namespace
@@ -1018,6 +1057,12 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     // cone of a pixel in one lane, so steps_px keeps one part
     k.split = (k.spec_on && k.nd > 0 && !a->steps_px && !(a->variant & 0x200)) ? 1 : 0;
     k.nd_half = (k.nd + 1) / 2;
+    k.spec_first = (a->variant & 0x2000) ? 1 : 0;
+    {   // variant bits 16-19: XCD map (0 default; 1 contiguous runs; 2..6: chunks of 1, 4, 16, 64, 256 units)
+        static const int g_of[7] = {0, 0, 1, 4, 16, 64, 256};
+        const uint32_t m = (a->variant >> 16) & 0xf;
+        k.xcd_g = g_of[m < 7 ? m : 0];
+    }
     k.sc_part = k.sc_cone = nullptr; k.sc_flag = nullptr; k.sc_px = 0;
     const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
@@ -1044,6 +1089,14 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     blocks *= 1u + (uint32_t)k.split;
     const uint32_t wgs = wg1 ? 64u : 256u;
     if (wg1) blocks *= 4u;
+    if (((a->variant >> 16) & 0xf) == 0) {
+        // default XCD chunk: whole 64x64 tiles (64 waves) for full frames; 64x16 strips
+        // for the small launches of a multi-GPU rank (measured: 1080p 1.60 -> 1.44 ms,
+        // 4K 6.91 -> 6.15 ms, one rank of 8: 0.288 -> 0.265 ms)
+        const uint32_t units_per_part = blocks / (k.split == 2 ? 3u : 1u + (uint32_t)k.split);
+        const uint32_t unit_g = wg1 ? 1u : 4u;      // a 16x16 block is 4 waves
+        k.xcd_g = (int)((units_per_part * unit_g >= 16384u ? 64u : 16u) / unit_g);
+    }
     // O32 instantiations need every level below 4 GiB: n <= 512
     const bool o32 = g.n <= 512;
 #define VCT_K4_WG(BRICK, MINW, UNION, WG)                                                               \
@@ -1077,6 +1130,12 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
 }  // namespace vct
 
 #if defined(VCT_DEBUG_COUNTERS) || defined(VCT_DEBUG_CLOCK)
+#ifdef VCT_DEBUG_CLOCK
+extern "C" int vct_debug_waves(unsigned long long* out, int n) {   // out[n][3]; n <= 1 << 18
+    if (n > kDbgWaves) n = kDbgWaves;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_wave), sizeof(unsigned long long) * 3 * n) == hipSuccess ? n : -1;
+}
+#endif
 extern "C" int vct_debug_counters(unsigned long long* out, int reset) {   // out[40]: 32 counters, 8 clocks
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(vct_dbg_time), sizeof(unsigned long long) * 8) != hipSuccess)
