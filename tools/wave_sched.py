@@ -19,7 +19,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "voxel-based-global-illumination_amd")
-os.environ["VCT_LIB"] = os.path.join(PKG, "vct", "libvct_hip_clk.so")
+os.environ["VCT_LIB"] = os.path.join(PKG, "vct", "libvct_hip_wv.so" if "--wv" in sys.argv else "libvct_hip_clk.so")
 sys.path[:0] = [REPO, PKG]
 
 
@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--variant", type=lambda x: int(x, 0), default=0)
     ap.add_argument("--slots", type=int, default=256 * 16)
+    ap.add_argument("--wv", action="store_true", help="timeline-only build (make wv), no phase clocks")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -113,7 +114,10 @@ def main():
     out["max_waves_on_one_cu(first 64 CUs)"] = mx
     out["waves_per_xcc"] = np.bincount(xcc, minlength=8).tolist()
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    np.save(os.path.join(REPO, "gpurun_out", f"waves_{a.scene}_{a.variant:#x}.npy"), buf[:int(used.max()) + 1])
+    out["xcd_last_end_us"] = [round(float(en[xcc == x].max()), 1) if (xcc == x).any() else 0.0 for x in range(8)]
+    out["xcd_sum_wave_ms"] = [round(float(dur[xcc == x].sum()) / 1e3, 1) for x in range(8)]
+    np.save(os.path.join(REPO, "gpurun_out", f"waves_{a.scene}_{a.variant:#x}{'_wv' if a.wv else ''}.npy"),
+            buf[:int(used.max()) + 1])
     print(json.dumps(out))
 
 

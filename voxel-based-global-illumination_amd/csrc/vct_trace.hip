@@ -42,7 +42,7 @@
 __device__ unsigned long long vct_dbg_ctr[32];
 __device__ unsigned long long vct_dbg_time[8];
 #endif
-#ifdef VCT_DEBUG_CLOCK
+#if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
 // per-wave (start, end) of the real-time counter (100 MHz, chip-wide), indexed by
 // blockIdx * waves-per-block + wave; tools/wave_sched.py replays schedules from it
 constexpr int kDbgWaves = 1 << 18;
@@ -857,7 +857,7 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     float4* lds = lds_all[BRICK && !WG1 ? wave : 0];
     PhaseClock pc;
     pc.start();
-#ifdef VCT_DEBUG_CLOCK
+#if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
     const unsigned long long wave_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     // lane -> pixel of the wave's 8x8 block in Morton order (MORTON; else row-major):
@@ -984,7 +984,7 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
         if (lane == 0 && wt) atomicAdd(k.texels_total, (unsigned long long)wt);
     }
     pc.flush();
-#ifdef VCT_DEBUG_CLOCK
+#if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
     {
         const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
         if (lane == 0 && wid < (uint32_t)kDbgWaves) {
@@ -1129,13 +1129,13 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
 
 }  // namespace vct
 
-#if defined(VCT_DEBUG_COUNTERS) || defined(VCT_DEBUG_CLOCK)
-#ifdef VCT_DEBUG_CLOCK
+#if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
 extern "C" int vct_debug_waves(unsigned long long* out, int n) {   // out[n][3]; n <= 1 << 18
     if (n > kDbgWaves) n = kDbgWaves;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_wave), sizeof(unsigned long long) * 3 * n) == hipSuccess ? n : -1;
 }
 #endif
+#if defined(VCT_DEBUG_COUNTERS) || defined(VCT_DEBUG_CLOCK)
 extern "C" int vct_debug_counters(unsigned long long* out, int reset) {   // out[40]: 32 counters, 8 clocks
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(vct_dbg_time), sizeof(unsigned long long) * 8) != hipSuccess)
