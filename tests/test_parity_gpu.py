@@ -439,10 +439,20 @@ def test_voxelize_sequence_resets_sparsely(gpu_ready, oracle_mod):
         assert np.array_equal(ao, ref["albedo_occ"]) and np.array_equal(nm, ref["normal"]), name
         assert np.array_equal(ctx.download_level(0), ref["r0"]), name
         assert np.array_equal(gpu_pyramid_flat(ctx), ref["pyr"]), name
+    # a dense level-0 upload in between: the next injection still equals the oracle's
+    rng = np.random.default_rng(9)
+    ctx.upload_level0(rng.random((n, n, n, 4)).astype(np.float32))
+    _, (v, i, m, k) = scene_arrays("atrium")
+    ctx.voxelize(v, i, m, k)
+    ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    ref = oracle_mod.pipeline(n, g0, E, v, i, m, k, scenes.LIGHT_DIR)
+    assert np.array_equal(ctx.download_level(0), ref["r0"])
     # an empty mesh clears the grid
     ctx.voxelize(np.zeros((0, 14), np.float32), np.zeros(0, np.uint32))
     ao, nm = ctx.download_voxels()
     assert not ao.any() and not nm.any()
+    ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    assert not ctx.download_level(0).any()
     ctx.close()
 
 

@@ -496,16 +496,19 @@ vct_status vct_upload_level0(vct_ctx* c, const float* host) {
     VCT_HIP(hipMemcpyAsync(c->grid.pyr, host, nv * 16, hipMemcpyHostToDevice, c->stream), "upload level0");
     VCT_HIP(hipStreamSynchronize(c->stream), "sync");
     c->grid.injected = true;
+    c->grid.l0_dense = true;
     c->grid.mipped = false;
     return VCT_OK;
 }
 
+// the caller may write level 0 through this pointer: the next K2 clears it whole
 vct_status vct_level0_device(vct_ctx* c, void** dptr, size_t* bytes) {
     if (!c || !dptr) return VCT_EINVAL;
     *dptr = c->grid.pyr;
     if (bytes) *bytes = (size_t)c->grid.n * c->grid.n * c->grid.n * 16;
     // the caller (e.g. an RCCL broadcast) writes level 0 behind our back
     c->grid.injected = true;
+    c->grid.l0_dense = true;
     c->grid.mipped = false;
     return VCT_OK;
 }
@@ -526,6 +529,7 @@ vct_status vct_set_level0_from_device(vct_ctx* c, const void* src) {
     const size_t nv = (size_t)c->grid.n * c->grid.n * c->grid.n;
     VCT_HIP(hipMemcpyAsync(c->grid.pyr, src, nv * 16, hipMemcpyDeviceToDevice, c->stream), "copy level0 in");
     c->grid.injected = true;
+    c->grid.l0_dense = true;
     c->grid.mipped = false;
     return VCT_OK;
 }

@@ -27,6 +27,7 @@ struct Grid {
     float4* normal = nullptr;        // [n^3] (unit normal, 0)
     unsigned long long* occ_bits = nullptr;  // [n^3 / 64] occupancy bitmask
     bool voxelized = false, injected = false, mipped = false;
+    bool l0_dense = false;   // level 0 was replaced densely (upload / device copy): K2 must clear it whole
 };
 
 struct Mesh {

@@ -268,7 +268,7 @@ __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__
 // n^3 x 64-B accumulators.  One wave per bitmask word.
 __global__ void __launch_bounds__(256) k1_clear(unsigned long long* __restrict__ occ_bits, size_t nv,
                                                 long long* __restrict__ accum, float4* __restrict__ albedo_occ,
-                                                float4* __restrict__ normal) {
+                                                float4* __restrict__ normal, float4* __restrict__ level0) {
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nv) return;
     const unsigned long long w = occ_bits[v >> 6];
@@ -279,6 +279,7 @@ __global__ void __launch_bounds__(256) k1_clear(unsigned long long* __restrict__
         a[0] = z; a[1] = z; a[2] = z; a[3] = z;
         albedo_occ[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         normal[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        level0[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // K2 wrote only occupied voxels
     }
     if ((threadIdx.x & 63) == 0) occ_bits[v >> 6] = 0ull;   // after every lane has read it (one wave)
 }
@@ -588,7 +589,7 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
 
     // sparse reset of the previous voxelization (accum / voxels / bits are zero elsewhere)
     hipLaunchKernelGGL(k1_clear, dim3((uint32_t)((nv + 255) / 256)), dim3(256), 0, s, g.occ_bits, nv, g.accum,
-                       g.albedo_occ, g.normal);
+                       g.albedo_occ, g.normal, g.pyr);
     if ((e = hipMemsetAsync(total, 0, 8, s)) != hipSuccess) return e;
     if (n_tri > 0) {
         hipLaunchKernelGGL(k1_tri_setup, dim3((n_tri + 255) / 256), dim3(256), 0, s,
@@ -625,7 +626,7 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
         return hipGetLastError();
     }
     // lists of the occupied and of the lit voxels (n^3 <= 2^30: 32-bit entries),
-    // coarse bits, level 0 zeroed; then one lane per occupied / lit voxel
+    // coarse bits; then one lane per occupied / lit voxel
     const size_t nwords = nv / 64;
     int cs = 0;
     while ((g.n >> cs) > 64) ++cs;
@@ -639,7 +640,12 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
     uint32_t* coarse = lit + nv;
     hipStream_t s = c->stream;
     if ((e = hipMemsetAsync(counts, 0, 8, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(g.pyr, 0, nv * sizeof(float4), s)) != hipSuccess) return e;
+    // level 0 is zero outside the occupied voxels (K1's reset clears what K2 wrote)
+    // unless a dense upload replaced it since
+    if (g.l0_dense) {
+        if ((e = hipMemsetAsync(g.pyr, 0, nv * sizeof(float4), s)) != hipSuccess) return e;
+        g.l0_dense = false;
+    }
     hipLaunchKernelGGL(k2_list, dim3((uint32_t)((nwords + 255) / 256)), dim3(256), 0, s, g.occ_bits, nwords, occ,
                        counts);
     hipLaunchKernelGGL(k2_coarse, dim3((cn * cn * cn + 255) / 256), dim3(256), 0, s, g.occ_bits, (int)g.n, cs,
