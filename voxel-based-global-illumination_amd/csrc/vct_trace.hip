@@ -257,7 +257,9 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
     for (int c = 0; c < 8; ++c) {
         const int x = xs[c & 1], y = ys[(c >> 1) & 1], z = zs[c >> 2];
         in[c] = (unsigned)x < (unsigned)nl && (unsigned)y < (unsigned)nl && (unsigned)z < (unsigned)nl;
-        idx[c] = (uint32_t)x + (uint32_t)nl * ((uint32_t)y + (uint32_t)nl * (uint32_t)z);
+        // 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate): nl <= 512 and y + nl z < 2^18
+        // for every in-range corner; an out-of-range corner's index is never read (in[c] = false)
+        idx[c] = (uint32_t)x + __umul24((uint32_t)nl, (uint32_t)y + __umul24((uint32_t)nl, (uint32_t)z));
     }
     const auto lv = [&] {
         if constexpr (UNIF) return level_view<O32>(k, l);
@@ -449,7 +451,7 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
     const int lane = threadIdx.x & 63;
     const int sx = be.ox + (lane & 3), sy = be.oy + ((lane >> 2) & 3), sz = be.oz + (lane >> 4);
     const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
-    const uint32_t gi = (uint32_t)sx + (uint32_t)nl * ((uint32_t)sy + (uint32_t)nl * (uint32_t)sz);
+    const uint32_t gi = (uint32_t)sx + __umul24((uint32_t)nl, (uint32_t)sy + __umul24((uint32_t)nl, (uint32_t)sz));
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const LevelView<O32> lv = level_view<O32>(k, l);
     Tex4 t;
@@ -489,7 +491,7 @@ __device__ __forceinline__ float4 brick_sample(const Corner& c, const BrickEntry
                                                const float4* __restrict__ lds) {
     float wc[8];
     corner_weights(c.fx, c.fy, c.fz, wc);
-    const float4* b = lds + ((c.ix - be.ox) + 4 * (c.iy - be.oy) + kBz * (c.iz - be.oz));
+    const float4* b = lds + ((c.ix - be.ox) + 4 * (c.iy - be.oy) + __mul24(kBz, c.iz - be.oz));
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (one_slot) {
         float4 v[8];
