@@ -16,6 +16,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "liboracle_vct.so")
+CPU_BACKEND = os.path.join(HERE, "_build", "libvct_cpu.so")   # include/vct.h on the oracle
 
 
 def build():

@@ -1,0 +1,477 @@
+/*
+ * vct_cpu_backend.c — include/vct.h implemented on the CPU oracle
+ * (TEST INFRASTRUCTURE ONLY; oracle/_build/libvct_cpu.so).
+ *
+ * "the same header is implemented by the CPU oracle backend and
+ * the HIP backend (one .so each)".  This is that CPU backend.  It lets a test
+ * drive one ABI-level call sequence through both libraries and compare, and it
+ * lets the CPU test suite exercise the boundary's state machine and error
+ * behaviour without a GPU.  It is never loaded by the product: the package
+ * loads libvct_hip.so only and fails loudly without it (vct/_lib.py); tests
+ * select this library explicitly.
+ *
+ * Semantics: every compute entry point calls the oracle restatement of SURVEY
+ * Appendix A (vct_oracle.c).  "Device" pointers are host pointers here, the
+ * stream is ignored and every call is synchronous.  The G-buffer ray caster
+ * restates the HIP caster (csrc/vct_frame.hip: pixel_ray, ray_tri,
+ * write_gbuffer) operation by operation; the binned pass returns the same
+ * G-buffer as the brute-force one (as the HIP one does), so both entry points
+ * run the brute-force loop.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/vct.h"
+#include "../include/vct_spec.h"
+#include "vct_oracle.h"
+
+struct vct_ctx {
+    vct_config cfg;
+    uint32_t n, L;
+    int aniso;
+    float *r0, *pyr;                /* level 0; levels 1..L (vo_pyramid_floats) */
+    float *albedo_occ, *normal;     /* resolved K1 voxels */
+    int64_t* sums;                  /* [n^3][6] */
+    uint32_t* counts;
+    float* tri;                     /* [n_tri][4][4]: v0, e1, e2, kd (as the HIP mesh records) */
+    uint32_t n_tri;
+    int voxelized, injected, mipped;
+    char err[256];
+};
+
+static vct_status fail(vct_ctx* c, vct_status s, const char* msg) {
+    if (c) snprintf(c->err, sizeof c->err, "%s", msg);
+    return s;
+}
+
+static int is_pow2(uint32_t n) { return n && !(n & (n - 1)); }
+
+uint32_t vct_abi_version(void) { return VCT_ABI_VERSION; }
+
+const char* vct_status_string(vct_status s) {
+    switch (s) {
+        case VCT_OK: return "VCT_OK";
+        case VCT_EINVAL: return "VCT_EINVAL";
+        case VCT_ENOMEM: return "VCT_ENOMEM";
+        case VCT_EDEVICE: return "VCT_EDEVICE";
+        case VCT_ECOMM: return "VCT_ECOMM";
+        case VCT_ESTATE: return "VCT_ESTATE";
+    }
+    return "VCT_UNKNOWN";
+}
+
+const char* vct_last_error(const vct_ctx* c) { return c ? c->err : "null context"; }
+
+void vct_destroy(vct_ctx* c) {
+    if (!c) return;
+    free(c->r0); free(c->pyr); free(c->albedo_occ); free(c->normal);
+    free(c->sums); free(c->counts); free(c->tri);
+    free(c);
+}
+
+vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
+    if (!cfg || !out) return VCT_EINVAL;
+    *out = NULL;
+    if (!is_pow2(cfg->n) || cfg->n < 4 || cfg->n > 1024) return VCT_EINVAL;
+    if (!(cfg->extent > 0.0f) || !isfinite(cfg->extent)) return VCT_EINVAL;
+    if (cfg->n_diffuse != 0 && cfg->n_diffuse != 1 && cfg->n_diffuse != 9 && cfg->n_diffuse != 16)
+        return VCT_EINVAL;
+    vct_ctx* c = (vct_ctx*)calloc(1, sizeof *c);
+    if (!c) return VCT_ENOMEM;
+    c->cfg = *cfg;
+    c->cfg.device = 0;
+    c->n = cfg->n;
+    c->L = 0;
+    while ((1u << (c->L + 1)) <= c->n) ++c->L;
+    c->aniso = cfg->aniso ? 1 : 0;
+    const size_t nv = (size_t)c->n * c->n * c->n;
+    c->r0 = (float*)calloc(nv * 4, sizeof(float));
+    c->pyr = (float*)calloc(vo_pyramid_floats(c->n, c->aniso) + 4, sizeof(float));
+    c->albedo_occ = (float*)calloc(nv * 4, sizeof(float));
+    c->normal = (float*)calloc(nv * 4, sizeof(float));
+    c->sums = (int64_t*)calloc(nv * 6, sizeof(int64_t));
+    c->counts = (uint32_t*)calloc(nv, sizeof(uint32_t));
+    if (!c->r0 || !c->pyr || !c->albedo_occ || !c->normal || !c->sums || !c->counts) {
+        vct_destroy(c);
+        return VCT_ENOMEM;
+    }
+    *out = c;
+    return VCT_OK;
+}
+
+vct_status vct_get_config(const vct_ctx* c, vct_config* out) {
+    if (!c || !out) return VCT_EINVAL;
+    *out = c->cfg;
+    return VCT_OK;
+}
+
+vct_status vct_set_stream(vct_ctx* c, void* s) { (void)s; return c ? VCT_OK : VCT_EINVAL; }
+vct_status vct_synchronize(vct_ctx* c) { return c ? VCT_OK : VCT_EINVAL; }
+
+/* ---- K1 ------------------------------------------------------------------- */
+static vct_status voxelize_common(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                                  const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
+                                  const float* kd4, uint32_t n_mat) {
+    if (!c) return VCT_EINVAL;
+    if (n_idx % 3 != 0) return fail(c, VCT_EINVAL, "n_idx must be a multiple of 3");
+    if (n_idx > 0 && (!verts || !idx)) return fail(c, VCT_EINVAL, "null vertex or index array");
+    if (stride < 12 || stride % 4 != 0) return fail(c, VCT_EINVAL, "vertex_stride < 12 or not a multiple of 4");
+    if (kd4 && n_mat == 0) return fail(c, VCT_EINVAL, "material_kd4 with n_materials == 0");
+    const size_t nv = (size_t)c->n * c->n * c->n;
+    const uint32_t n_tri = n_idx / 3;
+    memset(c->sums, 0, nv * 6 * sizeof(int64_t));
+    memset(c->counts, 0, nv * sizeof(uint32_t));
+    /* the mesh records the G-buffer caster reads (k1_tri_setup) */
+    free(c->tri);
+    c->tri = (float*)calloc((size_t)(n_tri ? n_tri : 1) * 16, sizeof(float));
+    if (!c->tri) return fail(c, VCT_ENOMEM, "mesh records");
+    c->n_tri = n_tri;
+    int bad = 0;
+    for (uint32_t t = 0; t < n_tri; ++t) {
+        const uint32_t vi[3] = {idx[3 * t], idx[3 * t + 1], idx[3 * t + 2]};
+        const uint32_t m = tri_mat ? tri_mat[t] : 0u;
+        if (vi[0] >= n_verts || vi[1] >= n_verts || vi[2] >= n_verts || (kd4 && m >= n_mat)) { bad = 1; continue; }
+        const float* p0 = (const float*)((const char*)verts + (size_t)vi[0] * stride);
+        const float* p1 = (const float*)((const char*)verts + (size_t)vi[1] * stride);
+        const float* p2 = (const float*)((const char*)verts + (size_t)vi[2] * stride);
+        float* r = c->tri + (size_t)t * 16;
+        r[0] = p0[0]; r[1] = p0[1]; r[2] = p0[2];
+        r[4] = p1[0] - p0[0]; r[5] = p1[1] - p0[1]; r[6] = p1[2] - p0[2];
+        r[8] = p2[0] - p0[0]; r[9] = p2[1] - p0[1]; r[10] = p2[2] - p0[2];
+        r[12] = kd4 ? kd4[4 * m] : 1.0f; r[13] = kd4 ? kd4[4 * m + 1] : 1.0f; r[14] = kd4 ? kd4[4 * m + 2] : 1.0f;
+    }
+    if (n_idx && vo_voxelize(c->n, c->cfg.aabb_min, c->cfg.extent, verts, stride, n_verts, idx, n_idx, tri_mat, kd4,
+                             n_mat, c->sums, c->counts) != 0)
+        bad = 1;
+    vo_resolve(c->n, c->sums, c->counts, c->albedo_occ, c->normal);
+    c->voxelized = 1;
+    c->injected = c->mipped = 0;
+    if (bad) return fail(c, VCT_EINVAL, "vertex or material index out of range");
+    return VCT_OK;
+}
+
+vct_status vct_voxelize(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts, const uint32_t* idx,
+                        uint32_t n_idx, const uint32_t* tri_mat, const float* kd4, uint32_t n_mat) {
+    return voxelize_common(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, n_mat);
+}
+
+vct_status vct_voxelize_device(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts, const uint32_t* idx,
+                               uint32_t n_idx, const uint32_t* tri_mat, const float* kd4, uint32_t n_mat) {
+    if (c && ((kd4 && ((uintptr_t)kd4 & 15)) || ((uintptr_t)verts & 3)))
+        return fail(c, VCT_EINVAL, "material_kd4 must be 16-byte and verts 4-byte aligned");
+    return voxelize_common(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, n_mat);
+}
+
+/* ---- K2 / K3 ---------------------------------------------------------------- */
+vct_status vct_inject_directional(vct_ctx* c, const float dir[3], const float color[3]) {
+    if (!c || !dir || !color) return VCT_EINVAL;
+    if (!c->voxelized) return fail(c, VCT_ESTATE, "inject before voxelize");
+    const float len = sqrtf((dir[0] * dir[0] + dir[1] * dir[1]) + dir[2] * dir[2]);
+    if (!(len > 0.0f) || !isfinite(len)) return fail(c, VCT_EINVAL, "zero or non-finite light direction");
+    vo_inject(c->n, c->albedo_occ, c->normal, dir, color, c->r0);
+    c->injected = 1;
+    c->mipped = 0;
+    return VCT_OK;
+}
+
+vct_status vct_build_mips(vct_ctx* c) {
+    if (!c) return VCT_EINVAL;
+    if (!c->injected) return fail(c, VCT_ESTATE, "build_mips before inject / upload_level0");
+    vo_build_mips(c->n, c->aniso, c->r0, c->pyr);
+    c->mipped = 1;
+    return VCT_OK;
+}
+
+/* ---- K4 ------------------------------------------------------------------- */
+uint32_t vct_tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
+    if (world == 0) world = 1;
+    const uint32_t total = ((w + VCT_TILE - 1) / VCT_TILE) * ((h + VCT_TILE - 1) / VCT_TILE);
+    if (rank >= world || total <= rank) return 0;
+    return (total - rank + world - 1) / world;
+}
+
+vct_status vct_trace_device(vct_ctx* c, const vct_trace_args* a) {
+    if (!c || !a) return VCT_EINVAL;
+    if (!c->mipped) return fail(c, VCT_ESTATE, "trace before build_mips");
+    if (!a->pos4 || !a->nrm4 || !a->alb4 || !a->diffuse4 || !a->spec4)
+        return fail(c, VCT_EINVAL, "null G-buffer or output pointer");
+    if (a->width == 0 || a->height == 0 || a->width > 65536 || a->height > 65536)
+        return fail(c, VCT_EINVAL, "bad frame size");
+    if (a->tile_world > 1 && a->tile_rank >= a->tile_world) return fail(c, VCT_EINVAL, "tile_rank >= tile_world");
+    if (((uintptr_t)a->cone_steps & 7) || ((uintptr_t)a->texel_fetches & 7))
+        return fail(c, VCT_EINVAL, "cone_steps / texel_fetches must be 8-byte aligned");
+    if (((uintptr_t)a->pos4 | (uintptr_t)a->nrm4 | (uintptr_t)a->alb4 | (uintptr_t)a->diffuse4 |
+         (uintptr_t)a->spec4) & 15)
+        return fail(c, VCT_EINVAL, "G-buffer / output pointers must be 16-byte aligned");
+    const uint32_t w = a->width, h = a->height, world = a->tile_world ? a->tile_world : 1;
+    const uint32_t rank = a->tile_world ? a->tile_rank : 0;
+    const size_t px = (size_t)w * h;
+    float* d = (float*)malloc(px * 16);
+    float* s = (float*)malloc(px * 16);
+    uint32_t* st = (uint32_t*)calloc(px, 4);
+    if (!d || !s || !st) { free(d); free(s); free(st); return fail(c, VCT_ENOMEM, "trace staging"); }
+    vo_trace_params p;
+    p.n = c->n;
+    memcpy(p.g0, c->cfg.aabb_min, sizeof p.g0);
+    p.extent = c->cfg.extent;
+    p.aniso = c->aniso;
+    p.n_diffuse = c->cfg.n_diffuse;
+    p.specular = c->cfg.specular ? 1u : 0u;
+    memcpy(p.eye, a->eye, sizeof p.eye);
+    vo_trace(&p, c->r0, c->pyr, a->pos4, a->nrm4, a->alb4, w, h, 1, d, s, st, 0);
+    /* this rank's tiles only (tile t -> rank t % world), frame or rank-compact layout */
+    const uint32_t tx = (w + VCT_TILE - 1) / VCT_TILE, ty = (h + VCT_TILE - 1) / VCT_TILE;
+    uint64_t steps = 0;
+    for (uint32_t t = rank, lt = 0; t < tx * ty; t += world, ++lt) {
+        const uint32_t ox = (t % tx) * VCT_TILE, oy = (t / tx) * VCT_TILE;
+        for (uint32_t py = 0; py < VCT_TILE; ++py)
+            for (uint32_t qx = 0; qx < VCT_TILE; ++qx) {
+                const uint32_t x = ox + qx, y = oy + py;
+                const int in = x < w && y < h;
+                const size_t src = in ? (size_t)y * w + x : 0;
+                if (!in && !a->tile_compact) continue;
+                const size_t o = a->tile_compact ? (size_t)lt * VCT_TILE * VCT_TILE + (size_t)py * VCT_TILE + qx : src;
+                static const float z4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                memcpy(a->diffuse4 + 4 * o, in ? d + 4 * src : z4, 16);
+                memcpy(a->spec4 + 4 * o, in ? s + 4 * src : z4, 16);
+                if (in) {
+                    if (a->steps_px) a->steps_px[src] = st[src];
+                    steps += st[src];
+                }
+            }
+    }
+    if (a->cone_steps) *a->cone_steps += steps;
+    if (a->texel_fetches) *a->texel_fetches += 0;   /* the oracle does not count texels */
+    free(d); free(s); free(st);
+    return VCT_OK;
+}
+
+vct_status vct_trace(vct_ctx* c, const float* pos4, const float* nrm4, const float* alb4, uint32_t w, uint32_t h,
+                     const float eye[3], float* diff4, float* spec4, uint32_t* steps_px, uint64_t* cone_steps) {
+    if (!c || !pos4 || !nrm4 || !alb4 || !eye || !diff4 || !spec4) return VCT_EINVAL;
+    if (!c->mipped) return fail(c, VCT_ESTATE, "trace before build_mips");
+    if (w == 0 || h == 0) return fail(c, VCT_EINVAL, "bad frame size");
+    vo_trace_params p;
+    p.n = c->n;
+    memcpy(p.g0, c->cfg.aabb_min, sizeof p.g0);
+    p.extent = c->cfg.extent;
+    p.aniso = c->aniso;
+    p.n_diffuse = c->cfg.n_diffuse;
+    p.specular = c->cfg.specular ? 1u : 0u;
+    memcpy(p.eye, eye, sizeof p.eye);
+    uint32_t* st = steps_px ? steps_px : (uint32_t*)calloc((size_t)w * h, 4);
+    if (!st) return fail(c, VCT_ENOMEM, "steps staging");
+    const uint64_t tot = vo_trace(&p, c->r0, c->pyr, pos4, nrm4, alb4, w, h, 1, diff4, spec4, st, 0);
+    if (!steps_px) free(st);
+    if (cone_steps) *cone_steps = tot;
+    return VCT_OK;
+}
+
+static void untile(const float* g, uint32_t planes, uint32_t w, uint32_t h, uint32_t world, float* const* frames) {
+    const uint32_t tx = (w + VCT_TILE - 1) / VCT_TILE;
+    const uint32_t maxt = vct_tiles_for_rank(w, h, 0, world);
+    for (uint32_t p = 0; p < planes; ++p)
+        for (uint32_t y = 0; y < h; ++y)
+            for (uint32_t x = 0; x < w; ++x) {
+                const uint32_t t = (y / VCT_TILE) * tx + x / VCT_TILE, rank = t % world, lt = t / world;
+                const size_t src = (((size_t)rank * planes + p) * maxt + lt) * (VCT_TILE * VCT_TILE) +
+                                   (size_t)(y % VCT_TILE) * VCT_TILE + (x % VCT_TILE);
+                memcpy(frames[p] + 4 * ((size_t)y * w + x), g + 4 * src, 16);
+            }
+}
+
+vct_status vct_untile_device(vct_ctx* c, const float* g, uint32_t w, uint32_t h, uint32_t world, float* frame4) {
+    if (!c || !g || !frame4 || w == 0 || h == 0) return VCT_EINVAL;
+    untile(g, 1, w, h, world ? world : 1, &frame4);
+    return VCT_OK;
+}
+
+vct_status vct_untile_planes_device(vct_ctx* c, const float* g, uint32_t planes, uint32_t w, uint32_t h,
+                                    uint32_t world, float* const* frames4) {
+    if (!c || !g || !frames4 || w == 0 || h == 0 || planes == 0 || planes > 4) return VCT_EINVAL;
+    for (uint32_t p = 0; p < planes; ++p)
+        if (!frames4[p]) return VCT_EINVAL;
+    untile(g, planes, w, h, world ? world : 1, frames4);
+    return VCT_OK;
+}
+
+/* ---- G-buffer: the HIP caster restated (csrc/vct_frame.hip) ----------------- */
+static float dot3(float ax, float ay, float az, float bx, float by, float bz) { return (ax * bx + ay * by) + az * bz; }
+
+static float ray_tri(const float* r, float px, float py, float pz, float dx, float dy, float dz) {
+    const float *v0 = r, *e1 = r + 4, *e2 = r + 8;
+    const float pvx = dy * e2[2] - dz * e2[1], pvy = dz * e2[0] - dx * e2[2], pvz = dx * e2[1] - dy * e2[0];
+    const float det = dot3(e1[0], e1[1], e1[2], pvx, pvy, pvz);
+    if (fabsf(det) < 1e-12f) return -1.0f;
+    const float inv = 1.0f / det;
+    const float tx = px - v0[0], ty = py - v0[1], tz = pz - v0[2];
+    const float u = dot3(tx, ty, tz, pvx, pvy, pvz) * inv;
+    if (u < 0.0f || u > 1.0f) return -1.0f;
+    const float qx = ty * e1[2] - tz * e1[1], qy = tz * e1[0] - tx * e1[2], qz = tx * e1[1] - ty * e1[0];
+    const float v = dot3(dx, dy, dz, qx, qy, qz) * inv;
+    if (v < 0.0f || u + v > 1.0f) return -1.0f;
+    return dot3(e2[0], e2[1], e2[2], qx, qy, qz) * inv;
+}
+
+static vct_status gbuffer(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough, float* pos4,
+                          float* nrm4, float* alb4) {
+    if (!c || !cam || !pos4 || !nrm4 || !alb4 || w == 0 || h == 0) return VCT_EINVAL;
+    if (!c->tri) return fail(c, VCT_ESTATE, "raycast before voxelize");
+    const float tan_half = tanf(cam->zoom_deg * 0.5f * 3.14159265358979f / 180.0f);
+    const float aspect = (float)w / (float)h;
+    const float *P = cam->position, *F = cam->front, *U = cam->up, *R = cam->right;
+    for (uint32_t y = 0; y < h; ++y)
+        for (uint32_t x = 0; x < w; ++x) {
+            const float ndx = (2.0f * ((float)x + 0.5f) / (float)w - 1.0f) * tan_half * aspect;
+            const float ndy = (1.0f - 2.0f * ((float)y + 0.5f) / (float)h) * tan_half;
+            float dx = F[0] + ndx * R[0] + ndy * U[0];
+            float dy = F[1] + ndx * R[1] + ndy * U[1];
+            float dz = F[2] + ndx * R[2] + ndy * U[2];
+            const float il = 1.0f / sqrtf(dot3(dx, dy, dz, dx, dy, dz));
+            dx *= il; dy *= il; dz *= il;
+            float best = INFINITY;
+            int hit = -1;
+            for (uint32_t t = 0; t < c->n_tri; ++t) {
+                const float tt = ray_tri(c->tri + (size_t)t * 16, P[0], P[1], P[2], dx, dy, dz);
+                if (tt > 0.0f && tt < best) { best = tt; hit = (int)t; }
+            }
+            const size_t p = (size_t)y * w + x;
+            const float depth = best * dot3(dx, dy, dz, F[0], F[1], F[2]);
+            if (hit < 0 || depth < cam->near_plane || depth > cam->far_plane) {
+                memset(pos4 + 4 * p, 0, 16);
+                memset(nrm4 + 4 * p, 0, 16);
+                alb4[4 * p] = alb4[4 * p + 1] = alb4[4 * p + 2] = 0.0f;
+                alb4[4 * p + 3] = rough;
+                continue;
+            }
+            const float *e1 = c->tri + (size_t)hit * 16 + 4, *e2 = e1 + 4, *kd = e1 + 8;
+            float nx = e1[1] * e2[2] - e1[2] * e2[1], ny = e1[2] * e2[0] - e1[0] * e2[2],
+                  nz = e1[0] * e2[1] - e1[1] * e2[0];
+            const float nl = sqrtf(dot3(nx, ny, nz, nx, ny, nz));
+            nx /= nl; ny /= nl; nz /= nl;
+            if (dot3(nx, ny, nz, dx, dy, dz) > 0.0f) { nx = -nx; ny = -ny; nz = -nz; }
+            pos4[4 * p] = P[0] + dx * best; pos4[4 * p + 1] = P[1] + dy * best; pos4[4 * p + 2] = P[2] + dz * best;
+            pos4[4 * p + 3] = 1.0f;
+            nrm4[4 * p] = nx; nrm4[4 * p + 1] = ny; nrm4[4 * p + 2] = nz; nrm4[4 * p + 3] = 0.0f;
+            alb4[4 * p] = kd[0]; alb4[4 * p + 1] = kd[1]; alb4[4 * p + 2] = kd[2]; alb4[4 * p + 3] = rough;
+        }
+    return VCT_OK;
+}
+
+vct_status vct_gbuffer_raycast_device(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
+                                      float* pos4, float* nrm4, float* alb4) {
+    return gbuffer(c, cam, w, h, rough, pos4, nrm4, alb4);
+}
+
+vct_status vct_gbuffer_raster_device(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough,
+                                     float* pos4, float* nrm4, float* alb4) {
+    if (c && (uint64_t)w * h > 0x7fffffffull) return fail(c, VCT_EINVAL, "raster: frame too large");
+    return gbuffer(c, cam, w, h, rough, pos4, nrm4, alb4);
+}
+
+vct_status vct_composite_device(vct_ctx* c, const float* pos4, const float* nrm4, const float* alb4,
+                                const float* diffuse4, const float* spec4, uint32_t w, uint32_t h,
+                                const float dir_to_light[3], const float color[3], float* out_linear4,
+                                uint32_t* out_rgba8) {
+    if (!c || !pos4 || !nrm4 || !alb4 || !diffuse4 || !spec4 || !dir_to_light || !color || w == 0 || h == 0)
+        return VCT_EINVAL;
+    if (!out_linear4 && !out_rgba8) return fail(c, VCT_EINVAL, "composite: no output");
+    if (!c->voxelized) return fail(c, VCT_ESTATE, "composite before voxelize");
+    const float len = sqrtf((dir_to_light[0] * dir_to_light[0] + dir_to_light[1] * dir_to_light[1]) +
+                            dir_to_light[2] * dir_to_light[2]);
+    if (!(len > 0.0f) || !isfinite(len)) return fail(c, VCT_EINVAL, "zero or non-finite light direction");
+    vo_composite(c->n, c->cfg.aabb_min, c->cfg.extent, c->albedo_occ, pos4, nrm4, alb4, diffuse4, spec4, w, h,
+                 dir_to_light, color, out_linear4, out_rgba8);
+    return VCT_OK;
+}
+
+/* ---- memory ("device" = host here) ------------------------------------------ */
+vct_status vct_device_alloc(vct_ctx* c, size_t bytes, void** dptr) {
+    if (!c || !dptr || bytes == 0) return VCT_EINVAL;
+    *dptr = aligned_alloc(256, (bytes + 255) & ~(size_t)255);
+    return *dptr ? VCT_OK : fail(c, VCT_ENOMEM, "alloc");
+}
+
+vct_status vct_device_free(vct_ctx* c, void* dptr) {
+    if (!c) return VCT_EINVAL;
+    free(dptr);
+    return VCT_OK;
+}
+
+vct_status vct_memcpy(vct_ctx* c, void* dst, const void* src, size_t bytes, int kind) {
+    if (!c || (!dst && bytes) || (!src && bytes) || kind < 0 || kind > 2) return VCT_EINVAL;
+    if (bytes) memmove(dst, src, bytes);
+    return VCT_OK;
+}
+
+/* ---- grid access ------------------------------------------------------------ */
+uint32_t vct_num_levels(const vct_ctx* c) { return c ? c->L + 1 : 0; }
+
+vct_status vct_level_dims(const vct_ctx* c, uint32_t level, uint32_t* n_l, uint32_t* n_faces) {
+    if (!c || level > c->L) return VCT_EINVAL;
+    if (n_l) *n_l = c->n >> level;
+    if (n_faces) *n_faces = (level == 0 || !c->aniso) ? 1 : VCT_NUM_FACES;
+    return VCT_OK;
+}
+
+vct_status vct_download_level(vct_ctx* c, uint32_t level, uint32_t face, float* host) {
+    if (!c || !host || level > c->L) return VCT_EINVAL;
+    const uint32_t faces = (level == 0 || !c->aniso) ? 1 : VCT_NUM_FACES;
+    if (face >= faces) return fail(c, VCT_EINVAL, "face out of range for level");
+    const size_t nl = c->n >> level, vl = nl * nl * nl;
+    if (level == 0) memcpy(host, c->r0, vl * 16);
+    else memcpy(host, c->pyr + vo_level_offset(c->n, c->aniso, level) + face * vl * 4, vl * 16);
+    return VCT_OK;
+}
+
+vct_status vct_upload_level0(vct_ctx* c, const float* host) {
+    if (!c || !host) return VCT_EINVAL;
+    memcpy(c->r0, host, (size_t)c->n * c->n * c->n * 16);
+    c->injected = 1;
+    c->mipped = 0;
+    return VCT_OK;
+}
+
+vct_status vct_level0_device(vct_ctx* c, void** dptr, size_t* bytes) {
+    if (!c || !dptr) return VCT_EINVAL;
+    *dptr = c->r0;
+    if (bytes) *bytes = (size_t)c->n * c->n * c->n * 16;
+    c->injected = 1;
+    c->mipped = 0;
+    return VCT_OK;
+}
+
+vct_status vct_copy_level0_to_device(vct_ctx* c, void* dst) {
+    if (!c || !dst) return VCT_EINVAL;
+    memcpy(dst, c->r0, (size_t)c->n * c->n * c->n * 16);
+    return VCT_OK;
+}
+
+vct_status vct_set_level0_from_device(vct_ctx* c, const void* src) {
+    if (!c || !src) return VCT_EINVAL;
+    memcpy(c->r0, src, (size_t)c->n * c->n * c->n * 16);
+    c->injected = 1;
+    c->mipped = 0;
+    return VCT_OK;
+}
+
+vct_status vct_download_voxels(vct_ctx* c, float* albedo_occ4, float* normal4) {
+    if (!c) return VCT_EINVAL;
+    if (!c->voxelized) return fail(c, VCT_ESTATE, "download_voxels before voxelize");
+    const size_t nv = (size_t)c->n * c->n * c->n;
+    if (albedo_occ4) memcpy(albedo_occ4, c->albedo_occ, nv * 16);
+    if (normal4) memcpy(normal4, c->normal, nv * 16);
+    return VCT_OK;
+}
+
+vct_status vct_download_accum(vct_ctx* c, int64_t* sums6, uint32_t* counts) {
+    if (!c) return VCT_EINVAL;
+    if (!c->voxelized) return fail(c, VCT_ESTATE, "download_accum before voxelize");
+    const size_t nv = (size_t)c->n * c->n * c->n;
+    if (sums6) memcpy(sums6, c->sums, nv * 6 * sizeof(int64_t));
+    if (counts) memcpy(counts, c->counts, nv * sizeof(uint32_t));
+    return VCT_OK;
+}

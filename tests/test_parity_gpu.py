@@ -488,3 +488,76 @@ def test_composite_matches_oracle(gpu_ready, oracle_mod, name, n):
     assert (pos[..., 3] != 0).any() and (ref_lin[..., :3] > 0).any()
     # the shadow term matters on these scenes: some lit-facing pixels are shadowed
     ctx.close()
+
+
+@pytest.mark.parametrize("name", ["atrium", "random"])
+def test_backends_agree(gpu_ready, oracle_mod, name):
+    """include/vct.h has two implementations, the HIP library (the
+    product) and the CPU oracle backend (oracle/_build/libvct_cpu.so, test only).
+    One call sequence through the same binding gives the same results from both:
+    K1 sums / voxels, K2 level 0, every K3 level and face, the G-buffer of the
+    ray caster and of the binned pass, the full-frame trace, a 2-rank compact
+    tile split + un-permute, and the composite (linear bit-exact, RGBA8 +-1)."""
+    import ctypes as C
+    import torch
+    from vct import Context, _lib, scenes
+    from vct.camera import Camera
+    cpu = _lib.bind(C.CDLL(oracle_mod.CPU_BACKEND))
+    s, (v, i, m, k) = scene_arrays(name)
+    n, w, h = 32, 96, 64
+    g0, E = scenes.grid_for_unit_box(n)
+    dev = torch.device("cuda")
+    ctxs = {"hip": Context(n, g0, E), "cpu": Context(n, g0, E, lib=cpu)}
+    ctxs["hip"].set_stream(torch.cuda.current_stream().cuda_stream)
+    for c in ctxs.values():
+        c.voxelize(v, i, m, k)
+        c.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+        c.build_mips()
+    a, b = ctxs["hip"], ctxs["cpu"]
+    for x, y in zip(a.download_accum(), b.download_accum()):
+        assert np.array_equal(x, y)
+    for x, y in zip(a.download_voxels(), b.download_voxels()):
+        assert np.array_equal(x, y)
+    for l in range(a.num_levels):
+        for f in range(a.level_dims(l)[1]):
+            assert np.array_equal(a.download_level(l, f), b.download_level(l, f)), (l, f)
+    cam = Camera()
+    # "device" buffers: torch on the GPU, numpy for the CPU backend
+    gh = [torch.empty((h, w, 4), device=dev) for _ in range(3)]
+    gc = [np.zeros((h, w, 4), np.float32) for _ in range(3)]
+    for fn in ("gbuffer_raycast_device", "gbuffer_raster_device"):
+        getattr(a, fn)(cam, w, h, scenes.ROUGHNESS, *gh)
+        getattr(b, fn)(cam, w, h, scenes.ROUGHNESS, *[t.ctypes.data for t in gc])
+        torch.cuda.synchronize()
+        for x, y in zip(gh, gc):
+            assert np.array_equal(x.cpu().numpy(), y), fn
+    dh, sh = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+    dc, sc = np.zeros((h, w, 4), np.float32), np.zeros((h, w, 4), np.float32)
+    ch, cc = torch.zeros(1, dtype=torch.int64, device=dev), np.zeros(1, np.int64)
+    a.trace_device(*gh, w, h, cam.position, dh, sh, cone_steps=ch)
+    b.trace_device(*[t.ctypes.data for t in gc], w, h, cam.position, dc.ctypes.data, sc.ctypes.data,
+                   cone_steps=cc.ctypes.data)
+    torch.cuda.synchronize()
+    assert np.array_equal(dh.cpu().numpy(), dc) and np.array_equal(sh.cpu().numpy(), sc)
+    assert int(ch.item()) == int(cc[0]) > 0
+    from vct.multi import tiles_for_rank
+    maxt = tiles_for_rank(w, h, 0, 2)
+    gth = torch.zeros((2, 2, maxt * 4096, 4), device=dev)
+    gtc = np.zeros((2, 2, maxt * 4096, 4), np.float32)
+    for r in range(2):
+        a.trace_device(*gh, w, h, cam.position, gth[r, 0], gth[r, 1], tile_rank=r, tile_world=2, tile_compact=True)
+        b.trace_device(*[t.ctypes.data for t in gc], w, h, cam.position, gtc[r, 0].ctypes.data,
+                       gtc[r, 1].ctypes.data, tile_rank=r, tile_world=2, tile_compact=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(gth.cpu().numpy(), gtc)
+    lin_h, rgb_h = torch.empty((h, w, 4), device=dev), torch.empty((h, w), dtype=torch.int32, device=dev)
+    lin_c, rgb_c = np.zeros((h, w, 4), np.float32), np.zeros((h, w), np.uint32)
+    a.composite_device(*gh, dh, sh, w, h, scenes.LIGHT_DIR, out_linear4=lin_h, out_rgba8=rgb_h)
+    b.composite_device(*[t.ctypes.data for t in gc], dc.ctypes.data, sc.ctypes.data, w, h, scenes.LIGHT_DIR,
+                       out_linear4=lin_c.ctypes.data, out_rgba8=rgb_c.ctypes.data)
+    torch.cuda.synchronize()
+    assert np.array_equal(lin_h.cpu().numpy(), lin_c)
+    bh = rgb_h.cpu().numpy().view(np.uint32).view(np.uint8).astype(int)
+    assert np.abs(bh - rgb_c.view(np.uint8).astype(int)).max() <= 1
+    for c in ctxs.values():
+        c.close()

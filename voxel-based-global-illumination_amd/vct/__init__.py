@@ -54,8 +54,10 @@ class Context:
     """One vct_ctx: grid + pyramid resident in HBM of one GPU."""
 
     def __init__(self, n: int, aabb_min, extent: float, aniso: bool = True, n_diffuse: int = 9,
-                 specular: bool = True, device: int = -1):
-        self.lib = _lib.load()
+                 specular: bool = True, device: int = -1, lib=None):
+        # lib: another implementation of include/vct.h bound with _lib.bind (tests use
+        # the CPU oracle backend); default: the in-tree HIP library, no fallback
+        self.lib = lib if lib is not None else _lib.load()
         cfg = VctConfig()
         cfg.n = n
         cfg.aabb_min = (C.c_float * 3)(*[float(x) for x in aabb_min])

@@ -83,7 +83,14 @@ def load() -> C.CDLL:
         raise FileNotFoundError(
             f"{LIB_PATH} is missing: build it with `make -C voxel-based-global-illumination_amd` "
             "(the VCT path has no CPU fallback)")
-    lib = C.CDLL(LIB_PATH)
+    _lib = bind(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def bind(lib: C.CDLL) -> C.CDLL:
+    """Declare the include/vct.h signatures on a loaded implementation of the
+    header (the HIP library; tests also bind the CPU oracle backend,
+    oracle/_build/libvct_cpu.so, explicitly -- the product never does)."""
     P = C.c_void_p
     u32, i32, f32 = C.c_uint32, C.c_int32, C.c_float
     sig = {
@@ -124,5 +131,4 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
     return lib
