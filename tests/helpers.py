@@ -41,3 +41,28 @@ def gpu_pyramid_flat(ctx) -> np.ndarray:
         for f in range(nf):
             parts.append(ctx.download_level(l, f).ravel())
     return np.concatenate(parts) if parts else np.zeros(0, np.float32)
+
+
+def write_obj(scene, directory, name="scene"):
+    """Wavefront OBJ + MTL of a vct.scenes.Scene (one `usemtl` group per material,
+    9-digit floats: float32 positions round-trip exactly).  -> path of the .obj"""
+    import os
+    v, i, m, k = scene.arrays()
+    tri = i.reshape(-1, 3)
+    lines = [f"mtllib {name}.mtl"]
+    for row in v:
+        lines.append("v %.9g %.9g %.9g" % (row[0], row[1], row[2]))
+    for mat in range(k.shape[0]):
+        sel = np.flatnonzero(m == mat)
+        if sel.size == 0:
+            continue
+        lines.append(f"usemtl m{mat}")
+        for t in sel:
+            a, b, c = tri[t] + 1
+            lines.append(f"f {a} {b} {c}")
+    with open(os.path.join(directory, f"{name}.obj"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    with open(os.path.join(directory, f"{name}.mtl"), "w") as f:
+        for mat in range(k.shape[0]):
+            f.write(f"newmtl m{mat}\nKd %.9g %.9g %.9g\n\n" % tuple(k[mat, :3]))
+    return os.path.join(directory, f"{name}.obj")

@@ -561,3 +561,55 @@ def test_backends_agree(gpu_ready, oracle_mod, name):
     assert np.abs(bh - rgb_c.view(np.uint8).astype(int)).max() <= 1
     for c in ctxs.values():
         c.close()
+
+
+def test_cpp_host_renderer_slot(gpu_ready, tmp_path):
+    """The C++ host (host/main.cpp: the reference's Engine loop with the
+    ConeTraceRenderer in its Renderer slot, OBJ loaded by the in-repo assimp-3.3
+    equivalent) renders frames on the GPU through the C-ABI: every frame takes the
+    same cone steps, a rerun writes the same image, and the step count matches the
+    Python binding's trace of the same scene (the C++ camera derives its vectors in
+    float, the Python one in double, so pixels may differ in the last bit)."""
+    import os
+    import re
+    import subprocess
+    import torch
+    from helpers import write_obj
+    from vct import Context, scenes
+    from vct.camera import Camera
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "voxel-based-global-illumination_amd", "build", "vct_headless")
+    assert os.path.exists(exe), "build the host with `make -C voxel-based-global-illumination_amd host`"
+    s = scenes.atrium()
+    obj = write_obj(s, str(tmp_path))
+    n, w, h = 64, 160, 120
+    runs = []
+    for r in range(2):
+        out = str(tmp_path / f"frame{r}.ppm")
+        p = subprocess.run([exe, obj, str(n), str(w), str(h), "3", out], capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        steps = [int(x) for x in re.findall(r"(\d+) cone steps", p.stdout)]
+        assert len(steps) == 3 and len(set(steps)) == 1 and steps[0] > 0, p.stdout
+        data = open(out, "rb").read()
+        assert data.startswith(f"P6\n{w} {h}\n255\n".encode())
+        img = np.frombuffer(data[len(f"P6\n{w} {h}\n255\n"):], np.uint8).reshape(h, w, 3)
+        runs.append((steps[0], img))
+    assert runs[0][0] == runs[1][0] and np.array_equal(runs[0][1], runs[1][1])
+    img = runs[0][1]
+    assert len(np.unique(img.reshape(-1, 3), axis=0)) > 100          # a shaded scene, not a clear
+    g0, E = scenes.grid_for_unit_box(n)
+    ctx = Context(n, g0, E)
+    ctx.voxelize(*s.arrays())
+    ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    ctx.build_mips()
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    gb = [torch.empty((h, w, 4), device=dev) for _ in range(3)]
+    cam = Camera()
+    ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)
+    d, sp = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.trace_device(*gb, w, h, cam.position, d, sp, cone_steps=cnt)
+    torch.cuda.synchronize()
+    assert abs(int(cnt.item()) - runs[0][0]) <= 0.01 * runs[0][0], (int(cnt.item()), runs[0][0])
+    ctx.close()
