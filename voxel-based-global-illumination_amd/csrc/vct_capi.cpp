@@ -143,6 +143,9 @@ vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
     if (e == hipSuccess) e = hipMemset(g.albedo_occ, 0, nv * sizeof(float4));
     if (e == hipSuccess) e = hipMemset(g.normal, 0, nv * sizeof(float4));
     if (e == hipSuccess) e = hipMemset(g.occ_bits, 0, (nv / 64) * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&g.occ_list, nv * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&g.occ_count, 256);
+    if (e == hipSuccess) e = hipMemset(g.occ_count, 0, 256);
     if (e == hipSuccess) {
         StepRow rows[kMaxStepRows];
         const float tau_d = cfg->n_diffuse == 16 ? VCT_TAN20 : VCT_TAN30;
@@ -172,6 +175,8 @@ void vct_destroy(vct_ctx* c) {
     if (g.albedo_occ) (void)hipFree(g.albedo_occ);
     if (g.normal) (void)hipFree(g.normal);
     if (g.occ_bits) (void)hipFree(g.occ_bits);
+    if (g.occ_list) (void)hipFree(g.occ_list);
+    if (g.occ_count) (void)hipFree(g.occ_count);
     if (g.accum) (void)hipFree(g.accum);
     if (c->k1_err) (void)hipFree(c->k1_err);
     if (c->mesh.tri) (void)hipFree(c->mesh.tri);

@@ -26,6 +26,8 @@ struct Grid {
     float4* albedo_occ = nullptr;    // [n^3] (albedo rgb, occupancy)
     float4* normal = nullptr;        // [n^3] (unit normal, 0)
     unsigned long long* occ_bits = nullptr;  // [n^3 / 64] occupancy bitmask
+    uint32_t* occ_list = nullptr;            // [n^3] the occupied voxels of the last K1 (k2_list order)
+    uint32_t* occ_count = nullptr;           // [1] entries of occ_list
     bool voxelized = false, injected = false, mipped = false;
     bool l0_dense = false;   // level 0 was replaced densely (upload / device copy): K2 must clear it whole
 };

@@ -263,37 +263,41 @@ __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__
     }
 }
 
-// Sparse reset before a voxelization: the records, voxels and bits the previous
-// one set (everything else is zero by the ctx invariant), so K1 never streams the
-// n^3 x 64-B accumulators.  One wave per bitmask word.
-__global__ void __launch_bounds__(256) k1_clear(unsigned long long* __restrict__ occ_bits, size_t nv,
+// Sparse reset before a voxelization: the records, voxels and level-0 texels of
+// the voxels the previous one occupied (its occupied list; everything else is
+// zero by the ctx invariant), so K1 never streams the n^3 x 64-B accumulators.
+// One lane per listed voxel (grid-stride, the count is on the device).
+__global__ void __launch_bounds__(256) k1_clear(const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list,
                                                 long long* __restrict__ accum, float4* __restrict__ albedo_occ,
                                                 float4* __restrict__ normal, float4* __restrict__ level0) {
-    const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= nv) return;
-    const unsigned long long w = occ_bits[v >> 6];
-    if (w == 0ull) return;                       // wave-uniform
-    if ((w >> (v & 63)) & 1ull) {
+    const uint32_t cnt = *n_list;
+    const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const longlong2 z = make_longlong2(0, 0);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
+        const size_t v = list[i];
         longlong2* a = (longlong2*)(accum + 8 * v);
-        const longlong2 z = make_longlong2(0, 0);
         a[0] = z; a[1] = z; a[2] = z; a[3] = z;
-        albedo_occ[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        normal[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        level0[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // K2 wrote only occupied voxels
+        albedo_occ[v] = z4;
+        normal[v] = z4;
+        level0[v] = z4;                          // K2 wrote only occupied voxels
     }
-    if ((threadIdx.x & 63) == 0) occ_bits[v >> 6] = 0ull;   // after every lane has read it (one wave)
 }
 
-// K1 resolve: accumulators -> albedo/occupancy, normal of the voxels K1 hit
-// (their bits; the other voxels stay zero)
-__global__ void __launch_bounds__(256) k1_resolve(const long long* __restrict__ accum, size_t nv,
-                                                  float4* __restrict__ albedo_occ,
-                                                  float4* __restrict__ normal,
-                                                  const unsigned long long* __restrict__ occ_bits) {
-    size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= nv) return;
-    const unsigned long long w = occ_bits[v >> 6];
-    if (!((w >> (v & 63)) & 1ull)) return;
+// K1 resolve: accumulators -> albedo/occupancy, normal of the voxels K1 hit (the
+// occupied list k2_list builds from their bits; the other voxels stay zero)
+__device__ __forceinline__ void resolve_voxel(const long long* __restrict__ accum, size_t v,
+                                              float4* __restrict__ albedo_occ, float4* __restrict__ normal);
+
+__global__ void __launch_bounds__(256) k1_resolve(const long long* __restrict__ accum,
+                                                  const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list,
+                                                  float4* __restrict__ albedo_occ, float4* __restrict__ normal) {
+    const uint32_t cnt = *n_list;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256)
+        resolve_voxel(accum, list[i], albedo_occ, normal);
+}
+
+__device__ __forceinline__ void resolve_voxel(const long long* __restrict__ accum, size_t v,
+                                              float4* __restrict__ albedo_occ, float4* __restrict__ normal) {
     long long s[7];
     {
         const longlong2* a = (const longlong2*)(accum + 8 * v);
@@ -587,9 +591,13 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
     unsigned long long* tiles = (unsigned long long*)(base + off_tiles);
     unsigned long long* total = (unsigned long long*)(base + off_total);
 
-    // sparse reset of the previous voxelization (accum / voxels / bits are zero elsewhere)
-    hipLaunchKernelGGL(k1_clear, dim3((uint32_t)((nv + 255) / 256)), dim3(256), 0, s, g.occ_bits, nv, g.accum,
-                       g.albedo_occ, g.normal, g.pyr);
+    // sparse reset of the previous voxelization (its occupied list), then the bits
+    const size_t nwords = nv / 64;
+    const uint32_t lb = (uint32_t)std::min<size_t>((nv + 255) / 256, 4096);
+    hipLaunchKernelGGL(k1_clear, dim3(lb), dim3(256), 0, s, g.occ_list, g.occ_count, g.accum, g.albedo_occ,
+                       g.normal, g.pyr);
+    if ((e = hipMemsetAsync(g.occ_bits, 0, nwords * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(g.occ_count, 0, 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(total, 0, 8, s)) != hipSuccess) return e;
     if (n_tri > 0) {
         hipLaunchKernelGGL(k1_tri_setup, dim3((n_tri + 255) / 256), dim3(256), 0, s,
@@ -612,8 +620,11 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
                                n_tri, total, (int)g.n, g.accum, g.occ_bits);
         }
     }
-    hipLaunchKernelGGL(k1_resolve, dim3((uint32_t)((nv + 255) / 256)), dim3(256), 0, s, g.accum, nv,
-                       g.albedo_occ, g.normal, g.occ_bits);
+    // the occupied list (kept for the next reset and for K2), then resolve it
+    hipLaunchKernelGGL(k2_list, dim3((uint32_t)((nwords + 255) / 256)), dim3(256), 0, s, g.occ_bits, nwords,
+                       g.occ_list, g.occ_count);
+    hipLaunchKernelGGL(k1_resolve, dim3(lb), dim3(256), 0, s, g.accum, g.occ_list, g.occ_count, g.albedo_occ,
+                       g.normal);
     return hipGetLastError();
 }
 
@@ -625,35 +636,31 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
                            g.albedo_occ, g.normal, g.occ_bits, (int)g.n, lx, ly, lz, cr, cg, cb, g.pyr);
         return hipGetLastError();
     }
-    // lists of the occupied and of the lit voxels (n^3 <= 2^30: 32-bit entries),
-    // coarse bits; then one lane per occupied / lit voxel
-    const size_t nwords = nv / 64;
+    // the occupied list is K1's (g.occ_list); the lit list, coarse bits here; then
+    // one lane per occupied / lit voxel (n^3 <= 2^30: 32-bit entries)
     int cs = 0;
     while ((g.n >> cs) > 64) ++cs;
     const uint32_t cn = g.n >> cs, ncw = (cn * cn * cn + 31) / 32;
     void* sp = nullptr;
-    hipError_t e = scratch_get(c, 4, 256 + nv * 4 * 2 + (size_t)ncw * 4, &sp);
+    hipError_t e = scratch_get(c, 4, 256 + nv * 4 + (size_t)ncw * 4, &sp);
     if (e != hipSuccess) return e;
-    uint32_t* counts = (uint32_t*)sp;            // [0] occupied, [1] lit
-    uint32_t* occ = (uint32_t*)((char*)sp + 256);
-    uint32_t* lit = occ + nv;
+    uint32_t* counts = (uint32_t*)sp;            // [0] lit
+    uint32_t* lit = (uint32_t*)((char*)sp + 256);
     uint32_t* coarse = lit + nv;
     hipStream_t s = c->stream;
-    if ((e = hipMemsetAsync(counts, 0, 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(counts, 0, 4, s)) != hipSuccess) return e;
     // level 0 is zero outside the occupied voxels (K1's reset clears what K2 wrote)
     // unless a dense upload replaced it since
     if (g.l0_dense) {
         if ((e = hipMemsetAsync(g.pyr, 0, nv * sizeof(float4), s)) != hipSuccess) return e;
         g.l0_dense = false;
     }
-    hipLaunchKernelGGL(k2_list, dim3((uint32_t)((nwords + 255) / 256)), dim3(256), 0, s, g.occ_bits, nwords, occ,
-                       counts);
     hipLaunchKernelGGL(k2_coarse, dim3((cn * cn * cn + 255) / 256), dim3(256), 0, s, g.occ_bits, (int)g.n, cs,
                        coarse);
     const uint32_t blocks = (uint32_t)std::min<size_t>((nv / 64 + 255) / 256 + 1, 4096);
-    hipLaunchKernelGGL(k2_shade, dim3(blocks), dim3(256), 0, s, occ, counts, g.normal, lx, ly, lz, lit, counts + 1,
-                       g.pyr);
-    hipLaunchKernelGGL(k2_walk, dim3(512), dim3(1024), 0, s, lit, counts + 1, coarse, cs,
+    hipLaunchKernelGGL(k2_shade, dim3(blocks), dim3(256), 0, s, g.occ_list, g.occ_count, g.normal, lx, ly, lz, lit,
+                       counts, g.pyr);
+    hipLaunchKernelGGL(k2_walk, dim3(512), dim3(1024), 0, s, lit, counts, coarse, cs,
                        g.albedo_occ, g.normal, g.occ_bits, (int)g.n, lx, ly, lz, cr, cg, cb, g.pyr);
     return hipGetLastError();
 }
