@@ -385,6 +385,7 @@ struct ConeCtl {                 // wave-uniform facts about one cone
 struct BrickEntry {
     int lvl;                     // staged level (-1 = empty)
     int ox, oy, oz;              // its origin
+    int zero;                    // every staged texel is +0: any sample from it is exactly (+0, +0, +0, +0)
 };
 // The cache holds the bricks of the step's two levels: `a` for level l0, `b`
 // for l0 + 1.  A cone's mip level never decreases, so when l0 advances by one
@@ -468,19 +469,33 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
     return t;
 }
 
-__device__ __forceinline__ void stage_store(int mode, const ConeCtl& cc, const Tex4& t, float4* __restrict__ lds) {
+__device__ __forceinline__ uint32_t bits4(float4 v) {
+    return __float_as_uint(v.x) | __float_as_uint(v.y) | __float_as_uint(v.z) | __float_as_uint(v.w);
+}
+
+// stores this lane's staging texel(s); returns true when every value it stored is +0
+__device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const Tex4& t, float4* __restrict__ lds) {
     const int lane = threadIdx.x & 63;
     float4* p = lds + ((lane & 15) + kBz * (lane >> 4));
+    uint32_t nz;
     if (mode == kIso) {
         p[0] = t.a;
+        nz = bits4(t.a);
     } else if (mode == kComb) {     // f0, f1, f2 = the x, y, z faces
-        p[0] = combine3(cc.uwx, cc.uwy, cc.uwz, t.a, t.b, t.c);
+        const float4 v = combine3(cc.uwx, cc.uwy, cc.uwz, t.a, t.b, t.c);
+        p[0] = v;
+        nz = bits4(v);
     } else {
         p[0] = t.a;
         p[kBlk] = t.b;
         p[2 * kBlk] = t.c;
-        if (cc.nfaces > 3) p[3 * kBlk] = t.d;
+        nz = bits4(t.a) | bits4(t.b) | bits4(t.c);
+        if (cc.nfaces > 3) {
+            p[3 * kBlk] = t.d;
+            nz |= bits4(t.d);
+        }
     }
+    return nz == 0u;
 }
 
 // D_l from a staged brick: corner 0 at `b`; faces mode reads the lane's own
@@ -562,7 +577,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     bool useA = bA.lvl == l0 && wall_in(amA, in_brick(cA, bA));
     bool stA = false;
     if (!useA && (modeA != kFaces || faces_ok)) {
-        BrickEntry nb;
+        BrickEntry nb{};
         nb.lvl = l0;
         if (brick_origin(cA, amA, cc.neg, nb)) {
             bA = nb;
@@ -577,7 +592,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         cB = level_corner(l1, qx, qy, qz);
         useB = bB.lvl == l1 && wall_in(amB, in_brick(cB, bB));
         if (!useB && (modeB != kFaces || faces_ok)) {
-            BrickEntry nb;
+            BrickEntry nb{};
             nb.lvl = l1;
             if (brick_origin(cB, amB, cc.neg, nb)) {
                 bB = nb;
@@ -588,22 +603,31 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     }
     VCT_DBG(useA ? (stA ? 2 : 3) : 1);
     pc.mark(1);
+    // a brick whose texels are all +0 (empty space) is marked: its samples are exactly
+    // zero (fmaf(w, +0, +0) = +0 through the whole trilinear chain), so hits on it skip
+    // the LDS reads and the FMAs
     if (stA && stB) {
         const Tex4 tA = stage_load<O32>(k, l0, bA, modeA, cc);
         const Tex4 tB = stage_load<O32>(k, l1, bB, modeB, cc);
-        stage_store(modeA, cc, tA, ldsA);
-        stage_store(modeB, cc, tB, ldsB);
+        const bool zA = stage_store(modeA, cc, tA, ldsA);
+        const bool zB = stage_store(modeB, cc, tB, ldsB);
+        bA.zero = bc.a.zero = wall(zA);
+        bB.zero = bc.b.zero = wall(zB);
         wave_lds_sync();
     } else if (stA || stB) {
         const int mode = stA ? modeA : modeB;
-        stage_store(mode, cc, stage_load<O32>(k, stA ? l0 : l1, stA ? bA : bB, mode, cc), stA ? ldsA : ldsB);
+        const bool z = wall(stage_store(mode, cc, stage_load<O32>(k, stA ? l0 : l1, stA ? bA : bB, mode, cc),
+                                        stA ? ldsA : ldsB));
+        if (stA) bA.zero = bc.a.zero = z;
+        else bB.zero = bc.b.zero = z;
         wave_lds_sync();
     }
     pc.mark(2);
     float4 sA = z4, sB = z4;
-    if (useA || useB) {
-        if (useA && active) sA = brick_sample<KL>(cA, bA, modeA != kFaces, bx, by, bz, wdx, wdy, wdz, ldsA);
-        if (useB && activeB) sB = brick_sample<KL>(cB, bB, modeB != kFaces, bx, by, bz, wdx, wdy, wdz, ldsB);
+    const bool readA = useA && !bA.zero, readB = useB && !bB.zero;
+    if (readA || readB) {
+        if (readA && active) sA = brick_sample<KL>(cA, bA, modeA != kFaces, bx, by, bz, wdx, wdy, wdz, ldsA);
+        if (readB && activeB) sB = brick_sample<KL>(cB, bB, modeB != kFaces, bx, by, bz, wdx, wdy, wdz, ldsB);
         wave_lds_sync();
     }
     pc.mark(3);
@@ -731,7 +755,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.dir_uniform = wall_in(vm, (wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz)) && cc.nfaces == 3;
     }
     BrickCache bc;
-    bc.a = bc.b = BrickEntry{-1, 0, 0, 0};
+    bc.a = bc.b = BrickEntry{-1, 0, 0, 0, 0};
     bc.flip = 0;
     for (int i = 0;; ++i) {
         float D, fr;
