@@ -62,7 +62,7 @@ def main():
         c = list(ctr)
         print(f"variant {v}: level-A brick {c[0]} / gather {c[1]} / staged {c[2]} / cache hit {c[3]}; "
               f"gathers per level: {c[4:15]}")
-        print(f"  level A adaptive {c[26]}; level B staged {c[27]} / adaptive {c[28]} / hit {c[29]} / gather {c[30]}")
+        print(f"  level-A brick samples: zero brick {c[17]} / nonzero {c[15]}")
         print(f"  gather reasons: faces not uniform {c[16]}; footprint span (level 0) <=3/<=5/<=9/more {c[18:22]}"
               f"; (level>0) {c[22:26]}")
         if a.clk:

@@ -625,6 +625,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     pc.mark(2);
     float4 sA = z4, sB = z4;
     const bool readA = useA && !bA.zero, readB = useB && !bB.zero;
+    if (useA) VCT_DBG(bA.zero ? 17 : 15);          // level-A samples from zero / nonzero bricks
     if (readA || readB) {
         if (readA && active) sA = brick_sample<KL>(cA, bA, modeA != kFaces, bx, by, bz, wdx, wdy, wdz, ldsA);
         if (readB && activeB) sB = brick_sample<KL>(cB, bB, modeB != kFaces, bx, by, bz, wdx, wdy, wdz, ldsB);
