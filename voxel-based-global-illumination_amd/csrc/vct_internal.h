@@ -51,8 +51,9 @@ struct vct_ctx {
     hipStream_t stream = nullptr;
     vct::Grid grid;
     vct::Mesh mesh;
-    vct::Scratch scratch[7];      // reusable scratch (0 trace host staging, 1 voxelize temps,
-                                  // 2-3 G-buffer bins, 4 K2 work list, 5-6 K4 cone-split hand-over)
+    vct::Scratch scratch[8];      // reusable scratch (0 trace host staging, 1 voxelize temps,
+                                  // 2-3 G-buffer bins, 4 K2 work list, 5-6 K4 cone-split hand-over,
+                                  // 7 K1 candidate bucket table)
     vct::StepRow* step_tab = nullptr;   // [kMaxStepRows] diffuse-cone step table (device)
     unsigned* spec_keys = nullptr;      // [2 * kSpecSlots]: specular table keys (~0u free), then states
     vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)

@@ -218,6 +218,19 @@ __device__ __forceinline__ bool tri_box_overlap(const float* __restrict__ q, flo
 }
 
 constexpr int kCandPerThread = 8;
+constexpr int kCandBucket = 512;                 // candidates per bucket of the triangle-lookup table
+
+// bucket b -> the triangle holding candidate b * kCandBucket (triangles whose
+// candidate range crosses a bucket start write it; a giant triangle writes many)
+__global__ void __launch_bounds__(256) k1_bucket_starts(const unsigned long long* __restrict__ offs, uint32_t n_tri,
+                                                        const unsigned long long* __restrict__ total_p,
+                                                        uint32_t* __restrict__ starts) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_tri) return;
+    const unsigned long long lo = offs[t], hi = t + 1 < n_tri ? offs[t + 1] : *total_p;
+    if (hi <= lo) return;                        // no candidates
+    for (unsigned long long b = (lo + kCandBucket - 1) / kCandBucket; b * kCandBucket < hi; ++b) starts[b] = t;
+}
 
 // one lane = kCandPerThread consecutive (triangle, voxel) candidates
 __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__ geom,
@@ -225,12 +238,15 @@ __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__
                                                      const unsigned long long* __restrict__ offs,
                                                      uint32_t n_tri, const unsigned long long* __restrict__ total_p,
                                                      int n, long long* __restrict__ accum,
-                                                     unsigned long long* __restrict__ occ_bits) {
+                                                     unsigned long long* __restrict__ occ_bits,
+                                                     const uint32_t* __restrict__ starts) {
     const unsigned long long total = *total_p;
     const unsigned long long c0 = ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x) * kCandPerThread;
     if (c0 >= total) return;
-    // upper_bound(offs, c0) - 1
-    uint32_t lo = 0, hi = n_tri;
+    // upper_bound(offs, c0) - 1, searched between the triangles of this bucket's start
+    // and the next bucket's start (a few steps instead of log2(n_tri) dependent loads)
+    const unsigned long long bk = c0 / kCandBucket, nbk = (total + kCandBucket - 1) / kCandBucket;
+    uint32_t lo = starts[bk], hi = bk + 1 < nbk ? starts[bk + 1] + 1 : n_tri;
     while (hi - lo > 1) {
         uint32_t mid = (lo + hi) >> 1;
         if (offs[mid] <= c0) lo = mid; else hi = mid;
@@ -580,7 +596,7 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
     size_t off_offs = off_cnt + 8 * (size_t)n_tri;
     size_t off_tiles = off_offs + 8 * (size_t)n_tri;
     size_t off_total = off_tiles + 8 * (size_t)(n_tiles + 1);
-    size_t bytes = off_total + 64;
+    size_t bytes = off_total + 64;           // the bucket table follows (sized once the total is known)
     void* sp;
     if ((e = scratch_get(c, 1, bytes, &sp)) != hipSuccess) return e;
     char* base = (char*)sp;
@@ -616,8 +632,14 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
             unsigned long long threads = (h_total + kCandPerThread - 1) / kCandPerThread;
             unsigned long long blocks = (threads + 255) / 256;
             if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+            const unsigned long long nbk = (h_total + kCandBucket - 1) / kCandBucket;
+            void* bp;
+            if ((e = scratch_get(c, 7, (size_t)nbk * 4, &bp)) != hipSuccess) return e;
+            uint32_t* starts = (uint32_t*)bp;
+            hipLaunchKernelGGL(k1_bucket_starts, dim3((n_tri + 255) / 256), dim3(256), 0, s, offs, n_tri, total,
+                               starts);
             hipLaunchKernelGGL(k1_candidates, dim3((uint32_t)blocks), dim3(256), 0, s, geom, fix, offs,
-                               n_tri, total, (int)g.n, g.accum, g.occ_bits);
+                               n_tri, total, (int)g.n, g.accum, g.occ_bits, starts);
         }
     }
     // the occupied list (kept for the next reset and for K2), then resolve it
