@@ -163,6 +163,15 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         assert np.array_equal(d.cpu().numpy(), ref["diffuse"]), f"variant {variant:#x} diffuse (no steps_px)"
         assert np.array_equal(sp.cpu().numpy(), ref["spec"]), f"variant {variant:#x} spec (no steps_px)"
         assert int(cnt[0]) == ref["cone_steps"]
+    # no counters at all: the form compiled without the counting instructions (the
+    # bench's timed launches), and 0x4000 = the counting form without counters
+    for variant in (0, 0x4000, 0x400, 0x800, 0x200, 0):
+        d = torch.full((h, w, 4), -1.0, device=dev)
+        sp = torch.full((h, w, 4), -1.0, device=dev)
+        ctx.trace_device(*gb, w, h, cam.position, d, sp, variant=variant)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), ref["diffuse"]), f"variant {variant:#x} diffuse (no counters)"
+        assert np.array_equal(sp.cpu().numpy(), ref["spec"]), f"variant {variant:#x} spec (no counters)"
     ctx.close()
 
 

@@ -713,8 +713,9 @@ __device__ __forceinline__ bool spec_table(const TraceK& k, float tau, unsigned 
 }
 
 // one cone, wave-synchronous (A.6); same arithmetic as march().  TAB: (t, D,
-// l0, fr) come from a step table (the diffuse one, or a specular one).
-template <bool O32, bool UNION, bool TAB, int KL>
+// l0, fr) come from a step table (the diffuse one, or a specular one).  CNT:
+// count steps and texel fetches (the launches that report them); else both stay 0.
+template <bool O32, bool UNION, bool TAB, int KL, bool CNT = true>
 __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, float ox, float oy, float oz,
                                                 float dx, float dy, float dz, float tau, float4& res,
                                                 uint32_t& texels, float4* __restrict__ lds, const StepRegs& tab,
@@ -792,15 +793,17 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
             if (two) s = blend(s, sample_level<O32>(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz), fr);
         }
         if (active) {
-            texels += (l0 == 0 || !k.aniso) ? 8u : 24u;
-            if (two) texels += k.aniso ? 24u : 8u;
+            if constexpr (CNT) {
+                texels += (l0 == 0 || !k.aniso) ? 8u : 24u;
+                if (two) texels += k.aniso ? 24u : 8u;
+            }
             const float oma = 1.0f - a;
             cr = fmaf(oma, s.x, cr);
             cg = fmaf(oma, s.y, cg);
             cb = fmaf(oma, s.z, cb);
             a = fmaf(oma, s.w, a);
             if constexpr (!TAB) t = t + VCT_STEP_SCALE * D;
-            ++steps;
+            if constexpr (CNT) ++steps;
         }
         pc.mark(5);
     }
@@ -832,8 +835,10 @@ __device__ __forceinline__ float4 ld_coherent(float4* p) {
 // ===========================================================================
 // S3: the split-2 instantiation.  WG1: one wave per workgroup (an 8x8 block): a
 // wave's LDS is released when that wave ends, not when the slowest of four has
+// CNT: the launch reports step / texel counts (steps_px, cone_steps, texel_fetches);
+// the timed frame loop passes none and runs the form without the counting VALU.
 template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true, bool S3 = false,
-          bool WG1 = true>
+          bool WG1 = true, bool CNT = true>
 __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     __shared__ float4 lds_all[BRICK && !WG1 ? 4 : 1][BRICK ? 2 * entry_slots<UNION>() : 1];
     // split: the grid is 2 or 3 parts over the same pixels, dispatched in
@@ -934,7 +939,7 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
             const float dy = (cn * ny + ct * Ty) + cb * By;
             const float dz = (cn * nz + ct * Tz) + cb * Bz;
             float4 res;
-            if constexpr (BRICK) steps += march_brick<O32, UNION, true, KL>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, tab, pc);
+            if constexpr (BRICK) steps += march_brick<O32, UNION, true, KL, CNT>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, tab, pc);
             else steps += march<O32>(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
             if (S3 && grp == 2) {                // second half: results go to the hand-over scratch
                 if (in_frame || k.compact) st_coherent(&k.sc_cone[(size_t)(c - c_lo) * k.sc_px + oidx], res);
@@ -960,9 +965,9 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
             float4 res;
             if constexpr (BRICK) {
                 if (spec_table(k, tau, wballot(valid), tab))
-                    steps += march_brick<O32, UNION, true, KL>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
+                    steps += march_brick<O32, UNION, true, KL, CNT>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
                 else
-                    steps += march_brick<O32, UNION, false, KL>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
+                    steps += march_brick<O32, UNION, false, KL, CNT>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
             } else {
                 steps += march<O32>(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
             }
@@ -1000,13 +1005,13 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     if (in_frame || k.compact) {
         if (wr_diff) k.diff[oidx] = dout;
         if (wr_spec) k.spec[oidx] = sout;
-        if (k.steps_px && in_frame) k.steps_px[pix] = steps;
+        if (CNT && k.steps_px && in_frame) k.steps_px[pix] = steps;
     }
-    if (k.steps_total) {
+    if (CNT && k.steps_total) {
         const uint32_t ws = wave_sum_u32(steps);
         if (lane == 0 && ws) atomicAdd(k.steps_total, (unsigned long long)ws);
     }
-    if (k.texels_total) {
+    if (CNT && k.texels_total) {
         const uint32_t wt = wave_sum_u32(texels);
         if (lane == 0 && wt) atomicAdd(k.texels_total, (unsigned long long)wt);
     }
@@ -1124,20 +1129,21 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         const uint32_t unit_g = wg1 ? 1u : 4u;      // a 16x16 block is 4 waves
         k.xcd_g = (int)((units_per_part * unit_g >= 16384u ? 64u : 16u) / unit_g);
     }
+    const bool counting = k.steps_px || k.steps_total || k.texels_total;
     // O32 instantiations need every level below 4 GiB: n <= 512
     const bool o32 = g.n <= 512;
-#define VCT_K4_WG(BRICK, MINW, UNION, WG)                                                               \
+#define VCT_K4_WG(BRICK, MINW, UNION, WG, CNT)                                                          \
     do {                                                                                               \
         if (k.split == 2) {                                                                            \
-            if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, true, WG>), dim3(blocks), dim3(wgs), 0, c->stream, k); \
-            else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, true, WG>), dim3(blocks), dim3(wgs), 0, c->stream, k);   \
-        } else if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, false, WG>), dim3(blocks), dim3(wgs), 0, c->stream, k); \
-        else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, false, WG>), dim3(blocks), dim3(wgs), 0, c->stream, k);    \
+            if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, true, WG, CNT>), dim3(blocks), dim3(wgs), 0, c->stream, k); \
+            else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, true, WG, CNT>), dim3(blocks), dim3(wgs), 0, c->stream, k);   \
+        } else if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, false, WG, CNT>), dim3(blocks), dim3(wgs), 0, c->stream, k); \
+        else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, false, WG, CNT>), dim3(blocks), dim3(wgs), 0, c->stream, k);    \
     } while (0)
 #define VCT_K4(BRICK, MINW, UNION)                                                                      \
     do {                                                                                               \
-        if (wg1) VCT_K4_WG(BRICK, MINW, UNION, true);                                                  \
-        else VCT_K4_WG(BRICK, MINW, UNION, false);                                                     \
+        if (wg1) VCT_K4_WG(BRICK, MINW, UNION, true, true);                                            \
+        else VCT_K4_WG(BRICK, MINW, UNION, false, true);                                               \
     } while (0)
     switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers; 2 bricks without the four-face union
         case 1: VCT_K4(false, 1, true); break;
@@ -1147,7 +1153,9 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
             if (k.split == 2) hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false, true>), dim3(blocks), dim3(wgs), 0, c->stream, k);
             else hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false>), dim3(blocks), dim3(wgs), 0, c->stream, k);
             break;
-        default: VCT_K4(true, VCT_K4_MIN_WAVES, true);
+        default:
+            if (counting || !wg1 || (a->variant & 0x4000)) VCT_K4(true, VCT_K4_MIN_WAVES, true);   // 0x4000: counting form
+            else VCT_K4_WG(true, VCT_K4_MIN_WAVES, true, true, false);   // no counters: the timed form
     }
 #undef VCT_K4
 #undef VCT_K4_WG
