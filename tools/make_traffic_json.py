@@ -20,7 +20,7 @@ def main():
     n, w, h = (int(x) for x in sys.argv[2:5])
     scene, gbuf, variant = sys.argv[5], sys.argv[6], int(sys.argv[7])
     out = sys.argv[8] if len(sys.argv) > 8 else os.path.join(REPO, "profiles", "traffic_k4.json")
-    s = json.loads(subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), d, "k4_trace"],
+    s = json.loads(subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), d, os.environ.get("KSEL", "k4_trace")],
                                   capture_output=True, text=True, check=True).stdout)
     rec = {
         "config": [n, w, h, scene, gbuf, variant, 1],
