@@ -173,9 +173,22 @@ def main():
         k2_ms = timed(lambda: ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR))
         ctx.copy_level0_to_device(level0)
     bcast_ms = 0.0
+    k2_rep_ms, k2_rep_match = k2_ms, True
     if world > 1:
         dist.barrier()
         bcast_ms = timed(lambda: dist.broadcast(level0, src=0))
+        # SURVEY 8e alternative to the broadcast: every rank runs K2 itself (K2 is
+        # deterministic, so the replicated grid must equal the broadcast one bit for bit)
+        if rank != 0:
+            ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+            k2_rep_ms = timed(lambda: ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR))
+            mine = torch.empty_like(level0)
+            ctx.copy_level0_to_device(mine)
+            k2_rep_match = bool(torch.equal(mine, level0))
+            del mine
+        rep = torch.tensor([k2_rep_ms, 0.0 if k2_rep_match else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(rep, op=dist.ReduceOp.MAX)
+        k2_rep_ms, k2_rep_match = float(rep[0].item()), rep[1].item() == 0.0
         ctx.set_level0_from_device(level0)
     ctx.build_mips()
     k3_ms = timed(ctx.build_mips)
@@ -274,8 +287,13 @@ def main():
             "k2_inject_ms": round(k2_ms, 3),
             "k3_mips_ms": round(k3_ms, 3),
             "grid_bcast_ms": round(bcast_ms, 3),
-            # a frame whose light changes: inject + mips + trace (+ the broadcast at N > 1)
-            "frame_relight_ms": round(k2_ms + bcast_ms + k3_ms + ms_per_step, 3),
+            # a frame whose light changes: inject + mips + trace; at N > 1 the level-0 grid
+            # either comes from rank 0 by broadcast or every rank injects it itself
+            # (report the cheaper, keep the broadcast path); both are listed
+            "frame_relight_ms": round(min(k2_ms + bcast_ms, k2_rep_ms) + k3_ms + ms_per_step, 3),
+            "frame_relight_bcast_ms": round(k2_ms + bcast_ms + k3_ms + ms_per_step, 3),
+            "frame_relight_replicated_ms": round(k2_rep_ms + k3_ms + ms_per_step, 3),
+            "replicated_k2_equals_bcast": k2_rep_match,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
