@@ -116,6 +116,10 @@ def cpu_baseline(ctx, n, g0, E, gb_host, eye, n_diffuse, spec, steps_px_gpu, tar
     }
 
 
+# what each procedural scene stands in for (the reference's assets are not available offline)
+STAND_IN = {"atrium": " (Sponza stand-in)", "courtyard": " (San Miguel stand-in)"}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -271,7 +275,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic: procedural '{args.scene}' scene (Sponza stand-in), G_{args.gbuffer} G-buffer",
+            "data": f"synthetic: procedural '{args.scene}' scene{STAND_IN.get(args.scene, '')}, G_{args.gbuffer} G-buffer",
             "config": {
                 "workload": f"cone trace K4, {n}^3 aniso RGBA32F grid, {w}x{h}, "
                             f"{args.n_diffuse} diffuse + {1 if spec else 0} specular cones",

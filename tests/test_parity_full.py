@@ -1,9 +1,10 @@
-"""Parity at BASELINE.json's full configuration sizes (SURVEY.md 8a configs C2-C5).
+"""Parity at BASELINE.json's full configuration sizes (SURVEY.md 8a configs C1-C5).
 
 The C oracle finishes these sizes in seconds on the GPU box's host cores, so
 every config is checked against it on the whole frame, not on a scaled-down
 stand-in:
 
+* C1  Cornell box, 64^3, 1280x720, 1 diffuse cone, no specular;
 * C2  atrium ("Sponza" stand-in), 128^3, 1280x720, 9 diffuse cones, no specular;
 * C3  atrium, 256^3, 1920x1080, 9 diffuse + 1 specular (the bench / roofline run);
 * C4  atrium, 512^3, 3840x2160, 9 diffuse + 1 specular;
@@ -35,6 +36,7 @@ TRACE_TOL = 1e-3   # north_star: indirect-irradiance parity within 1e-3 relative
 
 CONFIGS = [
     # id, scene, n, w, h, n_diffuse, specular
+    ("C1", "cornell", 64, 1280, 720, 1, False),
     ("C2", "atrium", 128, 1280, 720, 9, False),
     ("C3", "atrium", 256, 1920, 1080, 9, True),
     ("C4", "atrium", 512, 3840, 2160, 9, True),
@@ -125,6 +127,12 @@ def test_full_config_parity(gpu_ready, oracle_mod, cid, name, n, w, h, nd, spec)
     ctx.trace_device(*gb, w, h, cam.position, d2, sp2, cone_steps=c2)
     torch.cuda.synchronize()
     assert torch.equal(d2, d) and torch.equal(sp2, sp) and int(c2.item()) == int(cnt.item())
+    # ... and so does the timed launch (no counters: the form without the counting code)
+    d2.fill_(-1.0)
+    sp2.fill_(-1.0)
+    ctx.trace_device(*gb, w, h, cam.position, d2, sp2)
+    torch.cuda.synchronize()
+    assert torch.equal(d2, d) and torch.equal(sp2, sp)
     # multi-GPU screen tiles: every rank's compact tiles un-permuted == the frame
     from vct.multi import tiles_for_rank
     for world in (2, 4, 8):
