@@ -17,8 +17,10 @@ split).  Frames are pipelined as a renderer's frame loop would run them: the
 all-gather of frame f overlaps the trace of frame f+1 (vct.multi.FrameTracer);
 every timed step still traces, gathers and un-permutes one whole frame, and
 the pipeline is drained inside the timed region.  The level-0 grid is injected on rank 0 and broadcast
-(RCCL) before the timed region, as when the light changes; K1/K3 timings are
-reported beside the metric.
+(RCCL) before the timed region, as when the light changes; every other rank
+also injects it itself (the replicated alternative, checked bit-equal), and
+K1/K2/K3, the broadcast and both relit-frame times are reported beside the
+metric.
 
 value = cone steps of the frame (counted by the kernel; identical to the
 oracle's count, tests/test_parity_gpu.py) x K / max-over-ranks wall time.
