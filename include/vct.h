@@ -106,6 +106,24 @@ vct_status  vct_get_config(const vct_ctx* ctx, vct_config* out);
 vct_status  vct_set_stream(vct_ctx* ctx, void* hip_stream); /* NULL = default stream */
 vct_status  vct_synchronize(vct_ctx* ctx);
 
+/* ---- one process driving several GPUs (SURVEY.md 8b vct_create_multi) ----------
+ * For a host that cannot run one process per GPU (the reference host is one thread
+ * with one GL context: engine.h:7, engine.cpp:57).  Device r = (cfg->device + r) mod
+ * the device count, r < n_devices (more ranks than devices share devices).  The
+ * returned context is device 0's; its calls keep their single-device meaning, except:
+ *  - vct_build_mips first copies level 0 to the other devices over xGMI (peer copy,
+ *    the replicated grid of SURVEY 8e) when it changed, then builds mips on every device;
+ *  - vct_trace / vct_trace_device split the frame into 64x64 tiles (tile t -> device
+ *    t % n_devices); every device traces its tiles, the others copy theirs to device 0
+ *    (peer copies) and device 0 un-permutes them into the outputs.  Pointers are device
+ *    0's; the other devices read the G-buffer through peer access.  tile_world /
+ *    tile_compact must be 0.  Outputs and counters are bit-identical to one device.
+ *  - vct_synchronize waits for every device; vct_destroy releases every device.
+ * K1 and the G-buffer passes run on device 0 only.  In a process per GPU (torch /
+ * RCCL) use vct_create per rank instead. */
+vct_status  vct_create_multi(const vct_config* cfg, uint32_t n_devices, vct_ctx** out);
+uint32_t    vct_num_devices(const vct_ctx* ctx);   /* 1 for a vct_create context */
+
 /* ---- K1 conservative voxelization (A.2) --------------------------------
  * verts: host array of n_verts records of `vertex_stride` bytes whose first 12
  * bytes are the world position (the reference `Vertex`, stdafx.h:36-42, is a

@@ -30,6 +30,7 @@
 
 struct vct_ctx {
     vct_config cfg;
+    uint32_t ndev;        /* vct_create_multi: the ranks the frame is split over (traced here by one CPU) */
     uint32_t n, L;
     int aniso;
     float *r0, *pyr;                /* level 0; levels 1..L (vo_pyramid_floats) */
@@ -107,6 +108,17 @@ vct_status vct_get_config(const vct_ctx* c, vct_config* out) {
     *out = c->cfg;
     return VCT_OK;
 }
+
+/* multi-device context: the same state machine; the CPU traces every rank's tiles
+   itself, so the outputs are the single-device ones (as the HIP library's must be) */
+vct_status vct_create_multi(const vct_config* cfg, uint32_t n_devices, vct_ctx** out) {
+    if (!cfg || !out || n_devices < 1 || n_devices > 64) return VCT_EINVAL;
+    vct_status st = vct_create(cfg, out);
+    if (st == VCT_OK) (*out)->ndev = n_devices;
+    return st;
+}
+
+uint32_t vct_num_devices(const vct_ctx* c) { return c ? (c->ndev ? c->ndev : 1u) : 0u; }
 
 vct_status vct_set_stream(vct_ctx* c, void* s) { (void)s; return c ? VCT_OK : VCT_EINVAL; }
 vct_status vct_synchronize(vct_ctx* c) { return c ? VCT_OK : VCT_EINVAL; }
@@ -201,6 +213,8 @@ vct_status vct_trace_device(vct_ctx* c, const vct_trace_args* a) {
     if (a->width == 0 || a->height == 0 || a->width > 65536 || a->height > 65536)
         return fail(c, VCT_EINVAL, "bad frame size");
     if (a->tile_world > 1 && a->tile_rank >= a->tile_world) return fail(c, VCT_EINVAL, "tile_rank >= tile_world");
+    if (c->ndev > 1 && (a->tile_world > 1 || a->tile_compact))
+        return fail(c, VCT_EINVAL, "a multi-device context splits the frame itself (tile_world / tile_compact)");
     if (((uintptr_t)a->cone_steps & 7) || ((uintptr_t)a->texel_fetches & 7))
         return fail(c, VCT_EINVAL, "cone_steps / texel_fetches must be 8-byte aligned");
     if (((uintptr_t)a->pos4 | (uintptr_t)a->nrm4 | (uintptr_t)a->alb4 | (uintptr_t)a->diffuse4 |

@@ -153,3 +153,35 @@ def test_state_machine_and_errors(cpu_lib):
     with pytest.raises(VctError, match="EINVAL"):
         ctx.download_level(1, 6)                                             # face out of range
     ctx.close()
+
+
+def test_multi_device_context_cpu(cpu_lib, oracle_mod):
+    """vct_create_multi on the CPU backend: the same call sequence and status codes as
+    the HIP library (test_parity_gpu.py::test_multi_device_context); the CPU traces
+    every rank's tiles itself, so the frame equals the single-device one."""
+    from vct._lib import VctConfig, VctTraceArgs
+    cfg = VctConfig()
+    cfg.n, cfg.extent, cfg.n_diffuse = 16, 1.0, 9
+    h = C.c_void_p()
+    assert cpu_lib.vct_create_multi(C.byref(cfg), 0, C.byref(h)) == 1       # EINVAL: no device
+    assert cpu_lib.vct_create_multi(C.byref(cfg), 65, C.byref(h)) == 1      # EINVAL: too many
+    one, s, _, (g0, E) = _ctx(cpu_lib, 16)
+    multi, _, _, _ = _ctx(cpu_lib, 16, devices=3)
+    assert (one.num_devices, multi.num_devices) == (1, 3)
+    from vct.camera import Camera
+    from vct import scenes
+    cam = Camera()
+    pos, nrm, alb = scenes.raycast_numpy(s, cam, 40, 24)
+    a, b = one.trace(pos, nrm, alb, cam.position), multi.trace(pos, nrm, alb, cam.position)
+    for key in ("diffuse", "spec", "steps_px"):
+        assert np.array_equal(a[key], b[key]), key
+    args = VctTraceArgs()
+    buf = np.zeros(64 * 4 + 8, np.float32)
+    base = _ptr(buf) + (16 - _ptr(buf) % 16) % 16
+    args.pos4 = args.nrm4 = args.alb4 = args.diffuse4 = args.spec4 = base
+    args.width = args.height = 2
+    args.tile_world, args.tile_rank = 2, 0
+    assert cpu_lib.vct_trace_device(multi.h, C.byref(args)) == 1            # the context splits itself
+    assert cpu_lib.vct_trace_device(one.h, C.byref(args)) == 0
+    multi.close()
+    one.close()

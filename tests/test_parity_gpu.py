@@ -622,3 +622,55 @@ def test_cpp_host_renderer_slot(gpu_ready, tmp_path):
     torch.cuda.synchronize()
     assert abs(int(cnt.item()) - runs[0][0]) <= 0.01 * runs[0][0], (int(cnt.item()), runs[0][0])
     ctx.close()
+
+
+@pytest.mark.parametrize("devices", [1, 2, 3])
+def test_multi_device_context(gpu_ready, devices):
+    """vct_create_multi (one process, several GPUs): the frame split over
+    `devices` ranks -- each traces its 64x64 tiles, the others' tiles reach device 0 by
+    peer copies, device 0 un-permutes -- equals a single-device context bit for bit
+    (outputs, per-pixel steps, counters), through the host and the device entry points,
+    and after the light changes (level 0 re-sent to the other devices).  On a one-GPU
+    box the ranks share the device (device r = r mod device count), which exercises the
+    same copies and ordering."""
+    import torch
+    from vct import Context, VctError, scenes
+    n, w, h = 64, 200, 136            # partial tiles at the right and bottom edges
+    ref, s, (v, i, m, k), (g0, E) = gpu_pipeline(n, "atrium")
+    ctx = Context(n, g0, E, devices=devices)
+    assert ctx.num_devices == devices
+    ctx.voxelize(v, i, m, k)
+    (pos, nrm, alb), cam = _gbuf("scene", s, None, g0, E, w, h)
+    dev = torch.device("cuda")
+    gb = [torch.from_numpy(a).to(dev) for a in (pos, nrm, alb)]
+    for light in (scenes.LIGHT_DIR, (-0.4, 1.0, 0.3)):
+        for c in (ref, ctx):
+            c.inject_directional(light, scenes.LIGHT_COLOR)
+            c.build_mips()
+        for l in range(ref.num_levels):
+            for f in range(ref.level_dims(l)[1]):
+                assert np.array_equal(ctx.download_level(l, f), ref.download_level(l, f)), (l, f)
+        a, b = ref.trace(pos, nrm, alb, cam.position), ctx.trace(pos, nrm, alb, cam.position)
+        for key in ("diffuse", "spec", "steps_px"):
+            assert np.array_equal(a[key], b[key]), f"{devices} devices: {key} (host entry point)"
+        assert a["cone_steps"] == b["cone_steps"]
+        for counters in (True, False):
+            outs = []
+            for c in (ref, ctx):
+                d = torch.full((h, w, 4), -1.0, device=dev)
+                sp = torch.full((h, w, 4), -1.0, device=dev)
+                cnt = torch.zeros(2, dtype=torch.int64, device=dev) if counters else None
+                c.trace_device(*gb, w, h, cam.position, d, sp, cone_steps=cnt[0:1] if counters else None,
+                               texel_fetches=cnt[1:2] if counters else None)
+                c.synchronize()
+                outs.append((d, sp, cnt))
+            (d0, s0, c0), (d1, s1, c1) = outs
+            assert torch.equal(d0, d1) and torch.equal(s0, s1), f"{devices} devices: device entry point"
+            if counters:
+                assert torch.equal(c0, c1), (c0.tolist(), c1.tolist())
+    if devices > 1:
+        d = torch.empty((h, w, 4), device=dev)
+        with pytest.raises(VctError):
+            ctx.trace_device(*gb, w, h, cam.position, d, d.clone(), tile_rank=0, tile_world=2)
+    ctx.close()
+    ref.close()

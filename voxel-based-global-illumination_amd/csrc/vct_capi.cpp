@@ -165,8 +165,51 @@ vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
     return VCT_OK;
 }
 
+vct_status vct_create_multi(const vct_config* cfg, uint32_t n_devices, vct_ctx** out) {
+    if (!cfg || !out || n_devices < 1 || n_devices > 64) return VCT_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VCT_EDEVICE;
+    int d0 = cfg->device;
+    if (d0 < 0 && hipGetDevice(&d0) != hipSuccess) return VCT_EDEVICE;
+    if (d0 >= ndev) return VCT_EINVAL;
+    vct_config c0 = *cfg;
+    c0.device = d0;
+    vct_ctx* c = nullptr;
+    vct_status st = vct_create(&c0, &c);
+    if (st != VCT_OK) return st;
+    auto bail = [&](vct_status s) { vct_destroy(c); return s; };
+    if (hipEventCreateWithFlags(&c->ev, hipEventDisableTiming) != hipSuccess) return bail(VCT_EDEVICE);
+    for (uint32_t r = 1; r < n_devices; ++r) {
+        vct_config ci = *cfg;
+        ci.device = (int)((d0 + r) % (uint32_t)ndev);   // more ranks than devices: ranks share devices
+        vct_ctx* p = nullptr;
+        if ((st = vct_create(&ci, &p)) != VCT_OK) return bail(st);
+        c->peers.push_back(p);
+        if (hipSetDevice(p->device) != hipSuccess ||
+            hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess)
+            return bail(VCT_EDEVICE);
+        p->own_stream = true;
+        if (hipEventCreateWithFlags(&p->ev, hipEventDisableTiming) != hipSuccess) return bail(VCT_EDEVICE);
+        if (p->device != d0) {   // device r reads device 0's G-buffer and writes its steps_px pixels
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, p->device, d0) != hipSuccess || !can) return bail(VCT_EDEVICE);
+            hipError_t e = hipDeviceEnablePeerAccess(d0, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return bail(VCT_EDEVICE);
+            (void)hipGetLastError();
+        }
+    }
+    if (hipSetDevice(d0) != hipSuccess) return bail(VCT_EDEVICE);
+    *out = c;
+    return VCT_OK;
+}
+
+uint32_t vct_num_devices(const vct_ctx* c) { return c ? 1u + (uint32_t)c->peers.size() : 0u; }
+
 void vct_destroy(vct_ctx* c) {
     if (!c) return;
+    for (vct_ctx* p : c->peers) vct_destroy(p);
+    c->peers.clear();
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     else (void)hipDeviceSynchronize();
@@ -185,6 +228,8 @@ void vct_destroy(vct_ctx* c) {
     if (c->spec_rows) (void)hipFree(c->spec_rows);
     for (auto& s : c->scratch)
         if (s.p) (void)hipFree(s.p);
+    if (c->ev) (void)hipEventDestroy(c->ev);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -202,6 +247,10 @@ vct_status vct_set_stream(vct_ctx* c, void* stream) {
 
 vct_status vct_synchronize(vct_ctx* c) {
     if (!c) return VCT_EINVAL;
+    for (vct_ctx* p : c->peers) {
+        VCT_HIP(hipSetDevice(p->device), "hipSetDevice");
+        VCT_HIP(hipStreamSynchronize(p->stream), "hipStreamSynchronize (peer)");
+    }
     vct_status s = use_device(c);
     if (s != VCT_OK) return s;
     VCT_HIP(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
@@ -289,6 +338,7 @@ vct_status vct_inject_directional(vct_ctx* c, const float dir[3], const float co
     VCT_HIP(launch_inject(c, lx, ly, lz, color[0], color[1], color[2]), "inject");
     c->grid.injected = true;
     c->grid.mipped = false;
+    c->grid.l0_on_peers = false;
     return VCT_OK;
 }
 
@@ -297,6 +347,27 @@ vct_status vct_build_mips(vct_ctx* c) {
     if (!c->grid.injected) return fail(c, VCT_ESTATE, "build_mips before inject / upload_level0");
     vct_status st = use_device(c);
     if (st != VCT_OK) return st;
+    if (!c->peers.empty() && !c->grid.l0_on_peers) {
+        // the replicated grid: level 0 from device 0 to every other device
+        // over xGMI, ordered after the work queued on device 0 (K2)
+        const size_t bytes = (size_t)c->grid.n * c->grid.n * c->grid.n * sizeof(float4);
+        VCT_HIP(hipEventRecord(c->ev, c->stream), "event record");
+        for (vct_ctx* p : c->peers) {
+            VCT_HIP(hipSetDevice(p->device), "hipSetDevice");
+            VCT_HIP(hipStreamWaitEvent(p->stream, c->ev, 0), "stream wait");
+            VCT_HIP(hipMemcpyPeerAsync(p->grid.pyr, p->device, c->grid.pyr, c->device, bytes, p->stream),
+                    "level-0 peer copy");
+            p->grid.injected = true;
+            p->grid.l0_dense = true;
+        }
+        c->grid.l0_on_peers = true;
+    }
+    for (vct_ctx* p : c->peers) {
+        VCT_HIP(hipSetDevice(p->device), "hipSetDevice");
+        VCT_HIP(launch_mips(p), "mips (peer)");
+        p->grid.mipped = true;
+    }
+    if (!c->peers.empty() && (st = use_device(c)) != VCT_OK) return st;
     VCT_HIP(launch_mips(c), "mips");
     c->grid.mipped = true;
     return VCT_OK;
@@ -304,6 +375,79 @@ vct_status vct_build_mips(vct_ctx* c) {
 
 uint32_t vct_tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
     return tiles_for_rank(w, h, rank, world);
+}
+
+// K4 over the devices of a multi-device context (device-0 pointers in `a`).  Device r
+// traces the 64x64 tiles t with t % world == r into rank-compact planes: device 0
+// straight into slot 0 of a gather buffer on device 0, the others into their own HBM,
+// then one peer copy over xGMI each into their slot; device 0 waits for those copies
+// and un-permutes both planes into the caller's frame (vct_untile_planes_device).
+// Devices 1.. read the G-buffer and write their pixels of steps_px through peer access;
+// their step / texel counters are copied over and folded into the caller's.
+static vct_status trace_multi(vct_ctx* c, const vct_trace_args* a) {
+    if (a->tile_world > 1 || a->tile_compact)
+        return fail(c, VCT_EINVAL, "a multi-device context splits the frame itself (tile_world / tile_compact)");
+    const uint32_t world = 1 + (uint32_t)c->peers.size();
+    const uint32_t w = a->width, h = a->height;
+    const size_t npx = (size_t)tiles_for_rank(w, h, 0, world) * VCT_TILE * VCT_TILE;
+    const size_t slice = 2 * npx * sizeof(float4);          // one device's [diffuse | specular]
+    const bool counting = a->cone_steps || a->texel_fetches;
+    void* gp = nullptr;
+    void* cp = nullptr;
+    VCT_HIP(scratch_get(c, 8, world * slice, &gp), "gather buffer");
+    if (counting) {
+        VCT_HIP(scratch_get(c, 9, world * 16, &cp), "counter buffer");
+        VCT_HIP(hipMemsetAsync(cp, 0, world * 16, c->stream), "memset counters");
+    }
+    // the other devices start after everything queued on device 0 so far (the G-buffer,
+    // the previous call's untile of the gather buffer)
+    VCT_HIP(hipEventRecord(c->ev, c->stream), "event record");
+    for (uint32_t r = 1; r < world; ++r) {
+        vct_ctx* p = c->peers[r - 1];
+        VCT_HIP(hipSetDevice(p->device), "hipSetDevice");
+        VCT_HIP(hipStreamWaitEvent(p->stream, c->ev, 0), "stream wait");
+        void* tp = nullptr;
+        VCT_HIP(scratch_get(p, 8, slice + 16, &tp), "tile buffer (peer)");
+        unsigned long long* pc = (unsigned long long*)((char*)tp + slice);
+        if (counting) VCT_HIP(hipMemsetAsync(pc, 0, 16, p->stream), "memset counters (peer)");
+        vct_trace_args b = *a;
+        b.tile_rank = r;
+        b.tile_world = world;
+        b.tile_compact = 1;
+        b.diffuse4 = (float*)tp;
+        b.spec4 = (float*)tp + npx * 4;
+        b.cone_steps = a->cone_steps ? pc : nullptr;
+        b.texel_fetches = a->texel_fetches ? pc + 1 : nullptr;
+        VCT_HIP(launch_trace(p, &b), "trace (peer)");
+        VCT_HIP(hipMemcpyPeerAsync((char*)gp + r * slice, c->device, tp, p->device, slice, p->stream),
+                "tile peer copy");
+        if (counting)
+            VCT_HIP(hipMemcpyPeerAsync((char*)cp + 16 * r, c->device, pc, p->device, 16, p->stream),
+                    "counter peer copy");
+        VCT_HIP(hipEventRecord(p->ev, p->stream), "event record (peer)");
+    }
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    vct_trace_args b = *a;
+    b.tile_rank = 0;
+    b.tile_world = world;
+    b.tile_compact = 1;
+    b.diffuse4 = (float*)gp;
+    b.spec4 = (float*)gp + npx * 4;
+    VCT_HIP(launch_trace(c, &b), "trace");
+    for (vct_ctx* p : c->peers) VCT_HIP(hipStreamWaitEvent(c->stream, p->ev, 0), "stream wait (peer)");
+    if (counting)
+        VCT_HIP(launch_add_counters(c, (const unsigned long long*)cp, world, a->cone_steps, a->texel_fetches),
+                "fold counters");
+    float4* f[2] = {(float4*)a->diffuse4, (float4*)a->spec4};
+    VCT_HIP(launch_untile(c, (const float4*)gp, 2, w, h, world, f), "untile");
+    return VCT_OK;
+}
+
+static vct_status trace_any(vct_ctx* c, const vct_trace_args* a) {
+    if (!c->peers.empty()) return trace_multi(c, a);
+    VCT_HIP(launch_trace(c, a), "trace");
+    return VCT_OK;
 }
 
 vct_status vct_trace_device(vct_ctx* c, const vct_trace_args* a) {
@@ -322,8 +466,7 @@ vct_status vct_trace_device(vct_ctx* c, const vct_trace_args* a) {
         return fail(c, VCT_EINVAL, "G-buffer / output pointers must be 16-byte aligned");
     vct_status st = use_device(c);
     if (st != VCT_OK) return st;
-    VCT_HIP(launch_trace(c, a), "trace");
-    return VCT_OK;
+    return trace_any(c, a);
 }
 
 vct_status vct_trace(vct_ctx* c, const float* pos4, const float* nrm4, const float* alb4, uint32_t w,
@@ -359,7 +502,8 @@ vct_status vct_trace(vct_ctx* c, const float* pos4, const float* nrm4, const flo
     a.diffuse4 = ddif; a.spec4 = dspc;
     a.steps_px = steps_px ? dstp : nullptr;
     a.cone_steps = dtot;
-    VCT_HIP(launch_trace(c, &a), "trace");
+    st = trace_any(c, &a);
+    if (st != VCT_OK) return st;
     VCT_HIP(hipMemcpyAsync(diff4, ddif, px * 16, hipMemcpyDeviceToHost, c->stream), "download diffuse");
     VCT_HIP(hipMemcpyAsync(spec4, dspc, px * 16, hipMemcpyDeviceToHost, c->stream), "download spec");
     if (steps_px) VCT_HIP(hipMemcpyAsync(steps_px, dstp, px * 4, hipMemcpyDeviceToHost, c->stream), "download steps");
@@ -503,6 +647,7 @@ vct_status vct_upload_level0(vct_ctx* c, const float* host) {
     c->grid.injected = true;
     c->grid.l0_dense = true;
     c->grid.mipped = false;
+    c->grid.l0_on_peers = false;
     return VCT_OK;
 }
 
@@ -515,6 +660,7 @@ vct_status vct_level0_device(vct_ctx* c, void** dptr, size_t* bytes) {
     c->grid.injected = true;
     c->grid.l0_dense = true;
     c->grid.mipped = false;
+    c->grid.l0_on_peers = false;
     return VCT_OK;
 }
 
@@ -536,6 +682,7 @@ vct_status vct_set_level0_from_device(vct_ctx* c, const void* src) {
     c->grid.injected = true;
     c->grid.l0_dense = true;
     c->grid.mipped = false;
+    c->grid.l0_on_peers = false;
     return VCT_OK;
 }
 

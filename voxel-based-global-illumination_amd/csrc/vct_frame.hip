@@ -298,6 +298,18 @@ __global__ void __launch_bounds__(256) k_composite(CompK k) {
     if (k.rgba8) k.rgba8[i] = to8(fr) | (to8(fg) << 8) | (to8(fb) << 16) | (255u << 24);
 }
 
+__global__ void k_add_counters(const unsigned long long* __restrict__ src, uint32_t n, unsigned long long* dst0,
+                               unsigned long long* dst1) {
+    if (threadIdx.x != 0) return;
+    unsigned long long a = 0, b = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        a += src[2 * i];
+        b += src[2 * i + 1];
+    }
+    if (dst0) *dst0 += a;
+    if (dst1) *dst1 += b;
+}
+
 }  // namespace
 
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
@@ -319,6 +331,12 @@ hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t planes, ui
     k.max_tiles = (int)tiles_for_rank(w, h, 0, world);
     dim3 grid((w + 15) / 16, (h + 15) / 16, planes);
     hipLaunchKernelGGL(k_untile, grid, dim3(256), 0, c->stream, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_add_counters(vct_ctx* c, const unsigned long long* src, uint32_t n, unsigned long long* dst0,
+                               unsigned long long* dst1) {
+    hipLaunchKernelGGL(k_add_counters, dim3(1), dim3(64), 0, c->stream, src, n, dst0, dst1);
     return hipGetLastError();
 }
 

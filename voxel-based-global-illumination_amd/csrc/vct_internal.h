@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <vector>
 #include "../../include/vct.h"
 #include "vct_device.h"
 
@@ -30,6 +31,7 @@ struct Grid {
     uint32_t* occ_count = nullptr;           // [1] entries of occ_list
     bool voxelized = false, injected = false, mipped = false;
     bool l0_dense = false;   // level 0 was replaced densely (upload / device copy): K2 must clear it whole
+    bool l0_on_peers = false;   // multi-device: the other devices hold this level 0 (vct_build_mips copies it)
 };
 
 struct Mesh {
@@ -51,13 +53,19 @@ struct vct_ctx {
     hipStream_t stream = nullptr;
     vct::Grid grid;
     vct::Mesh mesh;
-    vct::Scratch scratch[8];      // reusable scratch (0 trace host staging, 1 voxelize temps,
+    vct::Scratch scratch[10];     // reusable scratch (0 trace host staging, 1 voxelize temps,
                                   // 2-3 G-buffer bins, 4 K2 work list, 5-6 K4 cone-split hand-over,
-                                  // 7 K1 candidate bucket table)
+                                  // 7 K1 candidate bucket table, 8 multi-device tiles / gather,
+                                  // 9 multi-device step counters)
     vct::StepRow* step_tab = nullptr;   // [kMaxStepRows] diffuse-cone step table (device)
     unsigned* spec_keys = nullptr;      // [2 * kSpecSlots]: specular table keys (~0u free), then states
     vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)
     int* k1_err = nullptr;              // device flag of vct_voxelize_device (index out of range)
+    // vct_create_multi: this context is device rank 0 and owns one context per
+    // further device (ranks 1..n-1); empty for a single-device context
+    std::vector<vct_ctx*> peers;
+    hipEvent_t ev = nullptr;            // cross-device ordering of the multi-device calls
+    bool own_stream = false;            // stream created by vct_create_multi (destroyed with the ctx)
     std::string err;
 };
 
@@ -86,6 +94,10 @@ hipError_t launch_raycast(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_
                           float4* pos, float4* nrm, float4* alb);
 
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world);
+// dst[j] += sum over i < n of src[2 i + j], j = 0, 1 (a NULL dst is skipped): the
+// multi-device trace folds the other devices' step / texel counters into the caller's
+hipError_t launch_add_counters(vct_ctx* c, const unsigned long long* src, uint32_t n, unsigned long long* dst0,
+                               unsigned long long* dst1);
 
 // K4 step table for aperture tau on an n^3 grid (rows until t > n*sqrt(3), then
 // one sentinel row with t = +inf); returns the row count incl. the sentinel, or

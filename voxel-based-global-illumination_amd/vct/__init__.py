@@ -54,9 +54,11 @@ class Context:
     """One vct_ctx: grid + pyramid resident in HBM of one GPU."""
 
     def __init__(self, n: int, aabb_min, extent: float, aniso: bool = True, n_diffuse: int = 9,
-                 specular: bool = True, device: int = -1, lib=None):
+                 specular: bool = True, device: int = -1, lib=None, devices: int = 0):
         # lib: another implementation of include/vct.h bound with _lib.bind (tests use
-        # the CPU oracle backend); default: the in-tree HIP library, no fallback
+        # the CPU oracle backend); default: the in-tree HIP library, no fallback.
+        # devices > 0: one context over that many GPUs (vct_create_multi; screen tiles
+        # traced on every device, gathered on device 0 by peer copies)
         self.lib = lib if lib is not None else _lib.load()
         cfg = VctConfig()
         cfg.n = n
@@ -67,9 +69,13 @@ class Context:
         cfg.specular = 1 if specular else 0
         cfg.device = device
         h = C.c_void_p()
-        st = self.lib.vct_create(C.byref(cfg), C.byref(h))
+        if devices > 0:
+            st = self.lib.vct_create_multi(C.byref(cfg), devices, C.byref(h))
+        else:
+            st = self.lib.vct_create(C.byref(cfg), C.byref(h))
         if st != 0:
             raise VctError(st, "vct_create failed (is a HIP device visible?)")
+        self.num_devices = int(self.lib.vct_num_devices(h))
         self.h = h
         self.n = n
         self.aniso = aniso
