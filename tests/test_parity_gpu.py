@@ -604,6 +604,12 @@ def test_cpp_host_renderer_slot(gpu_ready, tmp_path):
         img = np.frombuffer(data[len(f"P6\n{w} {h}\n255\n"):], np.uint8).reshape(h, w, 3)
         runs.append((steps[0], img))
     assert runs[0][0] == runs[1][0] and np.array_equal(runs[0][1], runs[1][1])
+    # the same host driving three device ranks through vct_create_multi: the same image
+    out = str(tmp_path / "frame_multi.ppm")
+    p = subprocess.run([exe, obj, str(n), str(w), str(h), "2", out, "3"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert [int(x) for x in re.findall(r"(\d+) cone steps", p.stdout)] == [runs[0][0]] * 2, p.stdout
+    assert open(out, "rb").read() == open(str(tmp_path / "frame0.ppm"), "rb").read()
     img = runs[0][1]
     assert len(np.unique(img.reshape(-1, 3), axis=0)) > 100          # a shaded scene, not a clear
     g0, E = scenes.grid_for_unit_box(n)

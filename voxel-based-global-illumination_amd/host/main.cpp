@@ -3,7 +3,8 @@
 // image, so the loop runs a fixed number of frames and
 // dumps the last one as a PPM instead of swapping buffers.
 //
-//   vct_headless <model.obj> [grid=256] [width=800] [height=600] [frames=5] [out.ppm]
+//   vct_headless <model.obj> [grid=256] [width=800] [height=600] [frames=5] [out.ppm] [devices=1]
+//   (devices > 1: one process drives that many GPUs through vct_create_multi)
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -15,7 +16,7 @@ using namespace vcthost;
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s model.obj [grid] [width] [height] [frames] [out.ppm]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s model.obj [grid] [width] [height] [frames] [out.ppm] [devices]\n", argv[0]);
         return 2;
     }
     ConeTraceSettings s;
@@ -24,6 +25,7 @@ int main(int argc, char** argv) {
     if (argc > 4) s.height = (uint32_t)std::atoi(argv[4]);
     const int frames = argc > 5 ? std::atoi(argv[5]) : 5;
     const std::string out = argc > 6 ? argv[6] : "vct_frame.ppm";
+    if (argc > 7) s.devices = (uint32_t)std::atoi(argv[7]);
     // grid AABB = [-1,1]^3 padded by one voxel (vct.scenes.grid_for_unit_box)
     s.extent = 2.0f * s.grid / (s.grid - 2);
     for (float& a : s.aabb_min) a = -s.extent / 2;

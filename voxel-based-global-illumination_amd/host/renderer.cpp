@@ -20,7 +20,8 @@ ConeTraceRenderer::ConeTraceRenderer(const std::string& model_name, const ConeTr
     cfg.n_diffuse = s.n_diffuse;
     cfg.specular = s.specular ? 1 : 0;
     cfg.device = -1;
-    if (!check(vct_create(&cfg, &ctx_), "vct_create")) return;
+    if (!check(s.devices > 1 ? vct_create_multi(&cfg, s.devices, &ctx_) : vct_create(&cfg, &ctx_), "vct_create"))
+        return;
     const size_t fb = (size_t)s.width * s.height * 16;
     for (auto& p : gb_)
         if (!check(vct_device_alloc(ctx_, fb, &p), "alloc gbuffer")) return;

@@ -33,6 +33,7 @@ struct ConeTraceSettings {
     float roughness = 0.1f;
     float aabb_min[3] = {-1.0f, -1.0f, -1.0f};
     float extent = 2.0f;
+    uint32_t devices = 1;                 // > 1: one context over that many GPUs (vct_create_multi)
 };
 
 class ConeTraceRenderer : public Renderer {
