@@ -154,7 +154,9 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         assert np.array_equal(st.cpu().numpy().astype(np.uint32), ref["steps_px"])
         assert int(cnt[0]) == ref["cone_steps"]
         assert int(cnt[1]) > 24 * int(cnt[0]) // 2   # >= 1 aniso level per step on average
-    for variant in (0, 1, 0x100, 0x200, 0x400, 0x800, 0x400, 0):
+    # bits 20-23: diffuse parts of the split (3, 4 -> 3 parts of 3 cones, 5, 9 -> one cone each)
+    for variant in (0, 1, 0x100, 0x200, 0x400, 0x800, 0x400, 0x300400, 0x400400, 0x500400, 0x900400, 0x900400,
+                    0x500400, 0):
         d = torch.full((h, w, 4), -1.0, device=dev)
         sp = torch.full((h, w, 4), -1.0, device=dev)
         cnt = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -165,7 +167,7 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         assert int(cnt[0]) == ref["cone_steps"]
     # no counters at all: the form compiled without the counting instructions (the
     # bench's timed launches), and 0x4000 = the counting form without counters
-    for variant in (0, 0x4000, 0x400, 0x800, 0x200, 0):
+    for variant in (0, 0x4000, 0x400, 0x800, 0x200, 0x500400, 0x300400, 0):
         d = torch.full((h, w, 4), -1.0, device=dev)
         sp = torch.full((h, w, 4), -1.0, device=dev)
         ctx.trace_device(*gb, w, h, cam.position, d, sp, variant=variant)

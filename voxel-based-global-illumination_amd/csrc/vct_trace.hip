@@ -131,12 +131,13 @@ struct TraceK {
     StepRow* spec_rows;          // [kSpecSlots][64]
     int spec_tabs;               // 0: specular cones always derive their steps per lane (variant bit 0x100)
     int split;                   // 0: one workgroup per 16x16 block traces every cone; 1: two (diffuse | specular);
-                                 // 2: three (diffuse cones [0, nd_half) | [nd_half, nd) | specular)
-    int nd_half;
+                                 // 2: ndp diffuse parts (cones [g * nd_chunk, ...)) | specular
+    int nd_chunk;                // split 2: diffuse cones per part (part g: [g * nd_chunk, (g + 1) * nd_chunk) & nd)
+    int ndp;                     // split 2: diffuse parts (>= 2), each followed in blockIdx order by the next
     int spec_first;              // split 1: the specular part is dispatched first (variant bit 0x2000)
     int xcd_g;                   // units per XCD chunk of the workgroup map (0 = one contiguous run per XCD)
-    float4* sc_part;             // split 2: [px] diffuse sum after cones [0, nd_half)  (per output index)
-    float4* sc_cone;             // split 2: [cone - nd_half][px] results of cones [nd_half, nd)
+    float4* sc_part;             // split 2: [px] diffuse sum after cones [0, nd_chunk)  (per output index)
+    float4* sc_cone;             // split 2: [cone - nd_chunk][px] results of cones [nd_chunk, nd)
     size_t sc_px;                // pixels per scratch plane
     unsigned* sc_flag;           // split 2: [block][wave] hand-over counter (0 between launches)
 };
@@ -843,14 +844,15 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     __shared__ float4 lds_all[BRICK && !WG1 ? 4 : 1][BRICK ? 2 * entry_slots<UNION>() : 1];
     // split: the grid is 2 or 3 parts over the same pixels, dispatched in
     // blockIdx order: split 1 = diffuse cones | specular cone; split 2 = diffuse
-    // cones [0, nd_half) | [nd_half, nd) | specular.  The parts are multiples of
+    // cones [0, c) | [c, 2c) | ... | specular (ndp diffuse parts of c = nd_chunk cones;
+    // two by default).  The parts are multiples of
     // 8 blocks, so a block's parts run on the same XCD (same L2).  Shorter waves:
     // the last waves of a launch (the tail when a rank traces few tiles) end
-    // sooner.  In split 2 the two diffuse halves hand over through global
-    // scratch: the first to finish leaves its data, the second completes the
-    // spec's cone-order sum (the same fmaf chain) and writes the output.
-    const uint32_t nb = S3 ? gridDim.x / 3u : (k.split ? gridDim.x >> 1 : gridDim.x);
-    const uint32_t part = blockIdx.x >= nb ? (blockIdx.x >= 2u * nb ? 2u : 1u) : 0u;
+    // sooner.  In split 2 the diffuse parts hand over through global scratch:
+    // each leaves its data, the last to finish completes the spec's cone-order
+    // sum (the same fmaf chain) and writes the output.
+    const uint32_t nb = S3 ? gridDim.x / (uint32_t)(k.ndp + 1) : (k.split ? gridDim.x >> 1 : gridDim.x);
+    const uint32_t part = S3 ? blockIdx.x / nb : (blockIdx.x >= nb ? 1u : 0u);
     const uint32_t b = blockIdx.x - part * nb;
     // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid.
     // The hardware hands workgroup b to XCD b & 7.  Units (waves with WG1, else
@@ -874,15 +876,15 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     const uint32_t rb = WG1 ? rbw >> 2 : rbw;                 // the 16x16 block
     const uint32_t wave = WG1 ? (rbw & 3u) : threadIdx.x >> 6;  // its 8x8 quarter
     const uint32_t lt = rb >> 4, sub = rb & 15;
-    int c_lo = 0, c_hi = k.nd, grp = 0;        // diffuse cones [c_lo, c_hi); grp 1/2: a half of split 2
+    int c_lo = 0, c_hi = k.nd, grp = 0;        // diffuse cones [c_lo, c_hi); grp g >= 1: diffuse part g - 1 of split 2
     bool do_spec = k.spec_on != 0, wr_diff = true, wr_spec = true;
     if (k.split == 1) {
         if ((part == 0) != (k.spec_first != 0)) { do_spec = false; wr_spec = false; }
         else { c_hi = 0; wr_diff = false; }
     } else if (S3) {
-        if (part == 2) { c_hi = 0; wr_diff = false; }
+        if (part == (uint32_t)k.ndp) { c_hi = 0; wr_diff = false; }
         else { do_spec = false; wr_spec = false; wr_diff = false; grp = (int)part + 1;
-               if (part == 0) c_hi = k.nd_half; else c_lo = k.nd_half; }
+               c_lo = (int)part * k.nd_chunk; c_hi = min(k.nd, c_lo + k.nd_chunk); }
     }
     const bool do_diff = c_hi > c_lo;
     const uint32_t lane = threadIdx.x & 63;
@@ -941,8 +943,8 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
             float4 res;
             if constexpr (BRICK) steps += march_brick<O32, UNION, true, KL, CNT>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, tab, pc);
             else steps += march<O32>(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
-            if (S3 && grp == 2) {                // second half: results go to the hand-over scratch
-                if (in_frame || k.compact) st_coherent(&k.sc_cone[(size_t)(c - c_lo) * k.sc_px + oidx], res);
+            if (S3 && grp >= 2) {                // later parts: results go to the hand-over scratch
+                if (in_frame || k.compact) st_coherent(&k.sc_cone[(size_t)(c - k.nd_chunk) * k.sc_px + oidx], res);
             } else {
                 ir = fmaf(wk, res.x, ir);
                 ig = fmaf(wk, res.y, ig);
@@ -975,8 +977,8 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
         }
     }
     if (S3 && grp != 0) {
-        // split 2 hand-over: leave this half's data, count in; the second wave of
-        // the pair (same block, same wave slot) finishes the cone-order sum
+        // split 2 hand-over: leave this part's data, count in; the last of the ndp
+        // waves (same block, same wave slot) finishes the cone-order sum
         const bool px_ok = in_frame || k.compact;
         if (grp == 1 && px_ok) st_coherent(&k.sc_part[oidx], make_float4(ir, ig, ib, occ));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the device-coherent stores have landed
@@ -984,14 +986,14 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
         uint32_t prev = 0;
         if (lane == 0) prev = atomicAdd(&k.sc_flag[wid], 1u);
         prev = (uint32_t)__builtin_amdgcn_readfirstlane((int)prev);
-        if (prev == 1u) {                         // the partner has counted in: its data is there
+        if (prev == (uint32_t)k.ndp - 1u) {      // every other part has counted in: its data is there
             float4 acc = make_float4(ir, ig, ib, occ);
-            if (grp == 2 && px_ok) acc = ld_coherent(&k.sc_part[oidx]);
+            if (grp != 1 && px_ok) acc = ld_coherent(&k.sc_part[oidx]);
             const float(*cones)[4] = cone_table(k.nd);
-            for (int c = k.nd_half; c < k.nd; ++c) {
+            for (int c = k.nd_chunk; c < k.nd; ++c) {
                 const float wk = cones[c][3];
                 float4 res = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                if (px_ok) res = ld_coherent(&k.sc_cone[(size_t)(c - k.nd_half) * k.sc_px + oidx]);
+                if (px_ok) res = ld_coherent(&k.sc_cone[(size_t)(c - k.nd_chunk) * k.sc_px + oidx]);
                 acc.x = fmaf(wk, res.x, acc.x);
                 acc.y = fmaf(wk, res.y, acc.y);
                 acc.z = fmaf(wk, res.z, acc.z);
@@ -1088,7 +1090,8 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     // 0x800 two parts; default by launch size); per-pixel step counts need every
     // cone of a pixel in one lane, so steps_px keeps one part
     k.split = (k.spec_on && k.nd > 0 && !a->steps_px && !(a->variant & 0x200)) ? 1 : 0;
-    k.nd_half = (k.nd + 1) / 2;
+    k.nd_chunk = (k.nd + 1) / 2;
+    k.ndp = 2;
     k.spec_first = (a->variant & 0x2000) ? 1 : 0;
     {   // variant bits 16-19: XCD map (0 default; 1 contiguous runs; 2..6: chunks of 1, 4, 16, 64, 256 units)
         static const int g_of[7] = {0, 0, 1, 4, 16, 64, 256};
@@ -1101,7 +1104,13 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     const bool wg1 = !(a->variant & 0x1000);    // 0x1000: four waves per workgroup
     uint32_t blocks = nlt * 16;
     if (k.split && k.nd > 1 && ((a->variant & 0x400) || (!(a->variant & 0x800) && blocks <= kSplit3MaxBlocks))) {
-        // three parts: hand-over scratch [part | cones nd_half..nd-1] per output pixel + flags
+        // ndp diffuse parts + the specular part (ndp = 2 unless variant bits 20-23 ask for
+        // more); hand-over scratch [part | cones nd_chunk..nd-1] per output pixel + flags
+        uint32_t ndp = (a->variant >> 20) & 0xfu;
+        ndp = ndp < 2u ? 2u : (ndp > (uint32_t)k.nd ? (uint32_t)k.nd : ndp);
+        const uint32_t chunk = ((uint32_t)k.nd + ndp - 1u) / ndp;
+        k.nd_chunk = (int)chunk;
+        k.ndp = (int)(((uint32_t)k.nd + chunk - 1u) / chunk);   // no empty part
         const size_t npx = k.compact ? (size_t)nlt * VCT_TILE * VCT_TILE : (size_t)a->width * a->height;
         const size_t fbytes = (size_t)blocks * 4 * sizeof(unsigned);
         const bool fresh = c->scratch[5].bytes < fbytes;    // flags: zeroed when allocated, then
@@ -1110,7 +1119,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         hipError_t e = scratch_get(c, 5, fbytes, &fp);
         if (e != hipSuccess) return e;
         if (fresh && (e = hipMemsetAsync(fp, 0, c->scratch[5].bytes, c->stream)) != hipSuccess) return e;
-        if ((e = scratch_get(c, 6, (size_t)(1 + k.nd - k.nd_half) * npx * sizeof(float4), &sp)) != hipSuccess)
+        if ((e = scratch_get(c, 6, (size_t)(1 + k.nd - k.nd_chunk) * npx * sizeof(float4), &sp)) != hipSuccess)
             return e;
         k.split = 2;
         k.sc_flag = (unsigned*)fp;
@@ -1118,14 +1127,15 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         k.sc_cone = k.sc_part + npx;
         k.sc_px = npx;
     }
-    blocks *= 1u + (uint32_t)k.split;
+    const uint32_t nparts = k.split == 2 ? (uint32_t)k.ndp + 1u : 1u + (uint32_t)k.split;
+    blocks *= nparts;
     const uint32_t wgs = wg1 ? 64u : 256u;
     if (wg1) blocks *= 4u;
     if (((a->variant >> 16) & 0xf) == 0) {
         // default XCD chunk: whole 64x64 tiles (64 waves) for full frames; 64x16 strips
         // for the small launches of a multi-GPU rank (measured: 1080p 1.60 -> 1.44 ms,
         // 4K 6.91 -> 6.15 ms, one rank of 8: 0.288 -> 0.265 ms)
-        const uint32_t units_per_part = blocks / (k.split == 2 ? 3u : 1u + (uint32_t)k.split);
+        const uint32_t units_per_part = blocks / nparts;
         const uint32_t unit_g = wg1 ? 1u : 4u;      // a 16x16 block is 4 waves
         k.xcd_g = (int)((units_per_part * unit_g >= 16384u ? 64u : 16u) / unit_g);
     }
