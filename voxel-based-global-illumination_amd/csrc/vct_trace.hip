@@ -624,6 +624,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         wave_lds_sync();
     }
     pc.mark(2);
+    __builtin_amdgcn_s_setprio(3);               // LDS sampling / FMAs issue ahead of other waves (A/B: -0.6 %)
     float4 sA = z4, sB = z4;
     const bool readA = useA && !bA.zero, readB = useB && !bB.zero;
     if (useA) VCT_DBG(bA.zero ? 17 : 15);          // level-A samples from zero / nonzero bricks
@@ -787,6 +788,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         float4 s;
         if (TAB || wall_in(am, l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
+            __builtin_amdgcn_s_setprio(0);       // default priority for the step head, brick geometry and staging
             s = step_bricks<O32, UNION, KL>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy,
                                         wdz, lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
