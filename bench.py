@@ -129,6 +129,9 @@ def main():
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        raise SystemExit(f"bench.py --gpus {args.gpus} runs one process per GPU: launch it with "
+                         f"python -m torch.distributed.run --nproc-per-node {args.gpus} (WORLD_SIZE is {world})")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; VCT_DIST_BACKEND=gloo rehearses the N>1 path with
