@@ -4,35 +4,54 @@
 Workload (BASELINE.json configs[2], the roofline run): 256^3 anisotropic
 RGBA32F grid, 1920x1080 G-buffer, 9 diffuse + 1 specular cone.  Sponza is not
 available offline, so the scene is the procedural "atrium" stand-in
-(vct.scenes.atrium) and the G-buffer is G_scene, ray-cast by the HIP caster
-from the reference camera (eye (0,0,3), yaw -90, 45 deg FOV; camera.h:14-18,
-assets.cpp:25).
+(vct.scenes.atrium) and the G-buffer is G_scene, rastered by the HIP G-buffer
+pass from the reference camera (eye (0,0,3), yaw -90, 45 deg FOV; camera.h:14-18,
+assets.cpp:25).  The 1 M-triangle "courtyard" (San Miguel stand-in, curved and
+bumpy surfaces) is measured at the same size beside it (`secondary`).
 
 One "step" = one frame of the cone-trace pass (K4) over the whole framebuffer:
 each rank traces its interleaved 64x64 tiles (tile t -> rank t % N) and, for
-N > 1, the indirect-irradiance + specular framebuffers are all-gathered over
-RCCL (one all-gather of the rank's [diffuse | specular] buffer) and
-un-permuted on every rank (strong scaling: the frame is fixed, the tiles are
-split).  Frames are pipelined as a renderer's frame loop would run them: the
-all-gather of frame f overlaps the trace of frame f+1 (vct.multi.FrameTracer);
-every timed step still traces, gathers and un-permutes one whole frame, and
-the pipeline is drained inside the timed region.  The level-0 grid is injected on rank 0 and broadcast
-(RCCL) before the timed region, as when the light changes; every other rank
-also injects it itself (the replicated alternative, checked bit-equal), and
-K1/K2/K3, the broadcast and both relit-frame times are reported beside the
-metric.
+N > 1, the frame is assembled on the presenting rank 0 (every rank sends
+exactly its own tiles over RCCL; `--exchange allgather` all-gathers to every
+rank instead) and un-permuted there (strong scaling: the frame is fixed, the
+tiles are split).  Frames are pipelined as a renderer's frame loop runs them:
+the exchange of frame f overlaps the trace of frame f+1 (vct.multi.FrameTracer);
+every timed step still traces, exchanges and un-permutes one whole frame, and
+the pipeline is drained inside the timed region.  The level-0 grid is injected
+on rank 0 and broadcast (RCCL) before the timed region, as when the light
+changes; every other rank also injects it itself (the replicated alternative,
+checked bit-equal); K1/K2/K3, the broadcast, the trace alone (slowest rank) and
+the exchange alone are reported beside the metric.
 
 value = cone steps of the frame (counted by the kernel; identical to the
 oracle's count, tests/test_parity_gpu.py) x K / max-over-ranks wall time.
+
+roofline: K4 is bound by instruction issue, not HBM.  The
+binding figure is the VALU issue rate: SQ_INSTS_VALU per launch (rocprofv3 PMC,
+profiles/k4_counters.json, valid only for the library build it was measured
+on: the file records the .so's sha256) / the live K4 time, against 1024 SIMDs x
+2.4 GHz / 2 cycles per wave64 VALU instruction.  Beside it: the measured HBM
+traffic (2 FETCH_SIZE + WRITE_SIZE, gfx950 correction) against 8 TB/s, the
+scalar issue rate, and the spec's algorithmic texel bytes (`gather_bytes`,
+served ~99 % by LDS / L1 / L2).
+
+`--gpus N` without WORLD_SIZE in the environment starts the N ranks itself
+(one child process per GPU, before anything touches a GPU).  `--dry-run`
+rehearses the N-rank plumbing on the CPU (gloo, a pattern-writing stand-in
+for the trace; nothing is measured, value = null).
 
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import math
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,9 +59,15 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "voxel-based-global-illumination_amd"))
 sys.path.insert(0, REPO)
 
+METRIC = "Mcone-steps/s at 256^3 grid, 1080p, 9 diffuse + 1 spec cone; 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SIMDS, CUS, CLOCK_GHZ = 1024, 256, 2.4
+VALU_PEAK_G = SIMDS * CLOCK_GHZ / 2.0      # wave64 VALU instructions / ns: one per 2 cycles per SIMD-32
+SALU_PEAK_G = CUS * CLOCK_GHZ              # one scalar instruction per cycle per CU
 BYTES_PER_TEXEL = 16       # RGBA32F
 BYTES_PER_VALID_PX = 80    # 48 B G-buffer read + 32 B output write
+LIB = os.path.join(REPO, "voxel-based-global-illumination_amd", "vct", "libvct_hip.so")
+PROFILE = os.path.join(REPO, "profiles", "k4_counters.json")
 
 
 def parse():
@@ -58,14 +83,139 @@ def parse():
     p.add_argument("--n-diffuse", type=int, default=9)
     p.add_argument("--no-spec", action="store_true")
     p.add_argument("--variant", type=int, default=0)
+    p.add_argument("--exchange", default="present", choices=["present", "allgather"],
+                   help="N > 1: assemble the frame on rank 0 (send/recv) or on every rank (all-gather)")
+    p.add_argument("--secondary", default="courtyard",
+                   help="second scene measured at the same size (empty or 'none': skip)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_k4.json"))
+    p.add_argument("--profile-json", default=PROFILE)
+    p.add_argument("--dry-run", action="store_true", help="CPU rehearsal of the rank plumbing (gloo), no GPU")
     return p.parse_args()
 
 
+# ---------------------------------------------------------------------------
+# launcher: `--gpus N` without a torch.distributed environment
+# ---------------------------------------------------------------------------
+def spawn_ranks(args) -> int:
+    """Start one child per rank (env RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*) and
+    wait; this process never touches a GPU.  Rank 0's stdout is the JSON line."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = None if r == 0 else subprocess.DEVNULL
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=out, start_new_session=False))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:     # one rank failed: the others would wait forever in a collective
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# roofline inputs
+# ---------------------------------------------------------------------------
+def lib_sha256() -> str | None:
+    try:
+        with open(LIB, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
+def profile_key(n, w, h, scene, gbuffer, nd, spec, variant, world):
+    return f"{n}^3 {w}x{h} {scene} G_{gbuffer} {nd}+{1 if spec else 0} v{variant} ranks{world}"
+
+
+def load_profile(path, key):
+    """The PMC record of the timed K4 form for this workload and THIS library build, or (None, reason)."""
+    try:
+        with open(path) as f:
+            prof = json.load(f)
+    except (OSError, ValueError) as e:
+        return None, f"no profile ({e.__class__.__name__})"
+    rec = prof.get(key)
+    if rec is None:
+        return None, f"no profile entry for '{key}'"
+    sha = lib_sha256()
+    if rec.get("lib_sha256") != sha:
+        return None, "profile measured on another library build"
+    return rec, None
+
+
+def roofline(rec, reason, k4_ms, texels, valid_px, profile_path, key):
+    gather = texels * BYTES_PER_TEXEL + valid_px * BYTES_PER_VALID_PX
+    t = k4_ms * 1e-3
+    out = {"bound": "issue", "achieved": None, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s", "frac": None,
+           "traffic": None, "gather_bytes": gather, "gather_GBs": round(gather / t / 1e9, 1),
+           "texel_fetches_per_launch": texels,
+           "peak_basis": "1024 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
+    if rec is None:
+        out["note"] = reason
+        return out
+    valu, salu = rec["SQ_INSTS_VALU"], rec["SQ_INSTS_SALU"]
+    hbm = rec["hbm_bytes_per_launch"]
+    v_ach = valu / t / 1e9
+    s_ach = salu / t / 1e9
+    h_ach = hbm / t / 1e9
+    out.update({
+        "achieved": round(v_ach, 1), "frac": round(v_ach / VALU_PEAK_G, 4), "traffic": hbm,
+        "valu_insts_per_launch": valu,
+        "salu": {"achieved": round(s_ach, 1), "peak": SALU_PEAK_G, "unit": "G SALU instr/s",
+                 "frac": round(s_ach / SALU_PEAK_G, 4), "insts_per_launch": salu},
+        "hbm": {"achieved": round(h_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(h_ach / HBM_PEAK_GBS, 4)},
+        "profile": f"{os.path.relpath(profile_path, REPO)}#{key}",
+        "profile_kernel_ms": rec.get("duration_ms"),
+    })
+    if out["hbm"]["frac"] > out["frac"]:          # name the resource that binds
+        out.update({"bound": "hbm", "achieved": round(h_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": out["hbm"]["frac"], "valu_frac": round(v_ach / VALU_PEAK_G, 4)})
+    return out
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the C oracle on a bounded sample of the same frame
+# ---------------------------------------------------------------------------
+def host_info():
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    model = platform.processor() or None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": int(omp) if omp and omp.isdigit() else None}
+
+
 def cpu_baseline(ctx, n, g0, E, gb_host, eye, n_diffuse, spec, steps_px_gpu, target_s):
-    """Oracle (C port, OpenMP) on a bounded row sample of the same frame."""
     import numpy as np
     from oracle import oracle as O
     O.build()
@@ -77,15 +227,15 @@ def cpu_baseline(ctx, n, g0, E, gb_host, eye, n_diffuse, spec, steps_px_gpu, tar
         for f in range(ctx.level_dims(l)[1]):
             parts.append(ctx.download_level(l, f).ravel())
     pyr = np.concatenate(parts)
-    try:
-        cores = min(16, len(os.sched_getaffinity(0)))
-    except AttributeError:
-        cores = min(16, os.cpu_count() or 1)
-    # probe on every 128th row, then size the sample to ~target_s
+    host = host_info()
+    # threads: the CPU share the pool gives this job (OMP_NUM_THREADS, 16 per GPU on the
+    # MI355X boxes, whose affinity mask shows the whole 256-thread machine), else every
+    # core in the affinity mask
+    cores = host["omp_num_threads"] or host["affinity_cpus"] or os.cpu_count() or 1
     probe_step = 128
     t0 = time.perf_counter()
-    pr = O.trace(n, g0, E, r0, pyr, pos, nrm, alb, eye, aniso=True, n_diffuse=n_diffuse, specular=spec,
-                 row_step=probe_step, threads=cores)
+    O.trace(n, g0, E, r0, pyr, pos, nrm, alb, eye, aniso=True, n_diffuse=n_diffuse, specular=spec,
+            row_step=probe_step, threads=cores)
     tp = max(time.perf_counter() - t0, 1e-3)
     rows_probe = len(range(0, h, probe_step))
     rows_target = max(1, int(rows_probe * target_s / tp))
@@ -113,8 +263,9 @@ def cpu_baseline(ctx, n, g0, E, gb_host, eye, n_diffuse, spec, steps_px_gpu, tar
         "unit": "Mcone-steps/s",
         "cores": cores,
         "kind": "port",
-        "sample": sample + "; C oracle -O3 x86-64-v3 OpenMP",
+        "sample": sample + "; C oracle -O3 x86-64-v3 OpenMP, one thread per core used",
         "steps_match_gpu": match,
+        "host": host,
     }
 
 
@@ -122,44 +273,76 @@ def cpu_baseline(ctx, n, g0, E, gb_host, eye, n_diffuse, spec, steps_px_gpu, tar
 STAND_IN = {"atrium": " (Sponza stand-in)", "courtyard": " (San Miguel stand-in)"}
 
 
+def max_over_ranks(torch, dist, dev, vals, world):
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0:
+        if args.gpus > 1:
+            sys.exit(spawn_ranks(args))     # before anything touches a GPU
+        world = 1
+    if args.gpus != world:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE is {world}: one process per GPU")
+    if args.dry_run:
+        return dry_run(args, world)
+    run(args, world)
+
+
+def dry_run(args, world):
+    """The N-rank plumbing on the CPU: gloo process group, the FrameTracer exchange in the
+    chosen mode with a pattern-writing stand-in trace, max-over-ranks timing, one JSON
+    line.  Checks the assembled frame exactly; measures nothing."""
     import numpy as np
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus != world:
-        raise SystemExit(f"bench.py --gpus {args.gpus} runs one process per GPU: launch it with "
-                         f"python -m torch.distributed.run --nproc-per-node {args.gpus} (WORLD_SIZE is {world})")
+    from vct.multi import FrameTracer, PatternContext
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; VCT_DIST_BACKEND=gloo rehearses the N>1 path with
-    # several ranks on one device (RCCL refuses two ranks per GPU)
-    backend = os.environ.get("VCT_DIST_BACKEND", "nccl")
-    ndev = max(1, torch.cuda.device_count())
-    dev_index = local_rank % ndev if backend != "nccl" else local_rank
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
-    local_rank = dev_index
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
+    w, h = args.width, args.height
+    dev = torch.device("cpu")
+    res = {}
+    for mode in ("present", "allgather"):
+        tr = FrameTracer(PatternContext(torch), torch, dist, w, h, rank, world, dev, mode=mode)
+        gb = (None, None, None)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            tr.step(gb, (0.0, 0.0, 3.0))
+        tr.drain()
+        el = max_over_ranks(torch, dist, dev, [time.perf_counter() - t0], world)[0]
+        ok = True
+        if tr.holds_frame:
+            ref = np.arange(w * h, dtype=np.float32).reshape(h, w, 1).repeat(4, 2)
+            ok = np.array_equal(tr.diff.numpy(), ref) and np.array_equal(tr.spec.numpy(), -ref)
+        ok = max_over_ranks(torch, dist, dev, [0.0 if ok else 1.0], world)[0] == 0.0
+        res[mode] = {"frame_ok": ok, "ms_per_step": round(el / args.steps * 1e3, 3)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": None, "unit": "Mcone-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32", "data": "dry run (CPU, gloo, pattern stand-in trace)",
+            "dry_run": True, "exchange": args.exchange, "exchange_check": res,
+            "config": {"workload": "rank plumbing only", "width": w, "height": h,
+                       "parallelism": f"screen-tiles x{world}"},
+            "trace_ms_max_rank": None, "gather_ms": None, "allgather_ms": None,
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
-    from vct import Context, scenes
+
+def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, counting_only=False):
+    """K1-K3 for `scene_name`, the G-buffer, one counting frame, then K timed frames."""
+    import numpy as np
+    from vct import scenes
     from vct.camera import Camera
     from vct.multi import FrameTracer, compact_index
-
     n, w, h = args.n, args.width, args.height
-    spec = not args.no_spec
-    g0, E = scenes.grid_for_unit_box(n)
-    ctx = Context(n, g0, E, aniso=True, n_diffuse=args.n_diffuse, specular=spec, device=local_rank)
-    stream = torch.cuda.current_stream()
-    ctx.set_stream(stream.cuda_stream)
-    scene = scenes.SCENES[args.scene]()
-    v, i, m, k = scene.arrays()
 
     def timed(fn):
         torch.cuda.synchronize()
@@ -168,21 +351,23 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t) * 1e3
 
+    scene = scenes.SCENES[scene_name]()
+    v, i, m, k = scene.arrays()
     # K1 on every rank (each process holds the scene, as the reference's loader does),
     # from device-resident geometry (the reference's meshes live in GL buffers);
     # K1-K3 are timed on a second call (the first one allocates their scratch)
     dgeo = (torch.from_numpy(v).to(dev), torch.from_numpy(i.astype(np.int32)).to(dev),
             torch.from_numpy(m.astype(np.int32)).to(dev), torch.from_numpy(k).to(dev))
     ctx.voxelize_device(*dgeo)
-    k1_ms = timed(lambda: ctx.voxelize_device(*dgeo))
+    r = {"k1_voxelize_ms": round(timed(lambda: ctx.voxelize_device(*dgeo)), 3)}
+    del dgeo
     level0 = torch.empty((n ** 3 * 4,), dtype=torch.float32, device=dev)
     k2_ms = 0.0
     if rank == 0:
         ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
         k2_ms = timed(lambda: ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR))
         ctx.copy_level0_to_device(level0)
-    bcast_ms = 0.0
-    k2_rep_ms, k2_rep_match = k2_ms, True
+    bcast_ms, k2_rep_ms, k2_rep_match = 0.0, k2_ms, True
     if world > 1:
         dist.barrier()
         bcast_ms = timed(lambda: dist.broadcast(level0, src=0))
@@ -195,12 +380,13 @@ def main():
             ctx.copy_level0_to_device(mine)
             k2_rep_match = bool(torch.equal(mine, level0))
             del mine
-        rep = torch.tensor([k2_rep_ms, 0.0 if k2_rep_match else 1.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(rep, op=dist.ReduceOp.MAX)
-        k2_rep_ms, k2_rep_match = float(rep[0].item()), rep[1].item() == 0.0
+        k2_rep_ms, mism = max_over_ranks(torch, dist, dev, [k2_rep_ms, 0.0 if k2_rep_match else 1.0], world)
+        k2_rep_match = mism == 0.0
         ctx.set_level0_from_device(level0)
+    del level0
     ctx.build_mips()
     k3_ms = timed(ctx.build_mips)
+    r.update({"k2_inject_ms": round(k2_ms, 3), "k3_mips_ms": round(k3_ms, 3), "grid_bcast_ms": round(bcast_ms, 3)})
 
     cam = Camera()
     eye = [float(x) for x in cam.position]
@@ -209,11 +395,11 @@ def main():
         ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)   # row f2, == the ray caster
     else:
         ao, nm = ctx.download_voxels()
-        host = scenes.gbuffer_rand(ao, nm, g0, E, w, h, seed=42)
+        host = scenes.gbuffer_rand(ao, nm, ctx.aabb_min, ctx.extent, w, h, seed=42)
         gb = tuple(torch.from_numpy(a).to(dev) for a in host)
     torch.cuda.synchronize()
 
-    tracer = FrameTracer(ctx, torch, dist, w, h, rank, world, dev)
+    tracer = FrameTracer(ctx, torch, dist, w, h, rank, world, dev, mode=args.exchange)
     # counting pass (same kernel, counters on): frame cone steps and texel fetches
     cnt = torch.zeros(2, dtype=torch.int64, device=dev)
     steps_px = torch.zeros((h, w), dtype=torch.int32, device=dev)
@@ -244,38 +430,88 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = max_over_ranks(torch, dist, dev, [elapsed], world)[0]
     k4_ms = [a.elapsed_time(b) for a, b in ev]
     k4_avg_ms = sum(k4_ms) / len(k4_ms)
     k4_med_ms = sorted(k4_ms)[len(k4_ms) // 2]
-
     ms_per_step = elapsed / args.steps * 1e3
-    value = frame_steps * args.steps / elapsed / 1e6
-    bytes_launch = local_texels * BYTES_PER_TEXEL + local_valid * BYTES_PER_VALID_PX
-    achieved = bytes_launch / (k4_avg_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("config") == [n, w, h, args.scene, args.gbuffer, args.variant, world]:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    r.update({
+        "value": frame_steps * args.steps / elapsed / 1e6, "ms_per_step": ms_per_step, "frame_cone_steps": frame_steps,
+        "valid_px": frame_valid, "k4_kernel_ms_avg": k4_avg_ms, "k4_kernel_ms_median": k4_med_ms,
+        "local_texels": local_texels, "local_valid": local_valid,
+        "frame_relight_ms": round(min(k2_ms + bcast_ms, k2_rep_ms) + k3_ms + ms_per_step, 3),
+        "frame_relight_bcast_ms": round(k2_ms + bcast_ms + k3_ms + ms_per_step, 3),
+        "frame_relight_replicated_ms": round(k2_rep_ms + k3_ms + ms_per_step, 3),
+        "replicated_k2_equals_bcast": k2_rep_match,
+        "_gb": gb, "_eye": eye, "_steps_px": steps_px,
+    })
+    if world > 1:
+        # the parts of a step alone (not overlapped): the slowest rank's trace, and each
+        # exchange form (RCCL send/recv to rank 0; all-gather to every rank) + its untile
+        r["trace_ms_max_rank"] = round(max_over_ranks(torch, dist, dev, [k4_avg_ms], world)[0], 4)
+        for mode, key in (("present", "gather_ms"), ("allgather", "allgather_ms")):
+            tx = tracer if mode == args.exchange else FrameTracer(ctx, torch, dist, w, h, rank, world, dev, mode=mode)
+            tx.trace_local(gb, eye, variant=args.variant)
+            tx.gather()
+            gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.steps)]
+            dist.barrier()
+            torch.cuda.synchronize()
+            for s in range(args.steps):
+                gev[s][0].record(stream)
+                tx.gather()
+                gev[s][1].record(stream)
+            torch.cuda.synchronize()
+            g_ms = sum(a.elapsed_time(b) for a, b in gev) / args.steps
+            r[key] = round(max_over_ranks(torch, dist, dev, [g_ms], world)[0], 4)
+            del tx
+    return r
+
+
+def run(args, world):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; VCT_DIST_BACKEND=gloo rehearses the N>1 path with
+    # several ranks on one device (RCCL refuses two ranks per GPU)
+    backend = os.environ.get("VCT_DIST_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
+    dev_index = local_rank % ndev if backend != "nccl" else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+
+    from vct import Context, scenes
+
+    n, w, h = args.n, args.width, args.height
+    spec = not args.no_spec
+    g0, E = scenes.grid_for_unit_box(n)
+    ctx = Context(n, g0, E, aniso=True, n_diffuse=args.n_diffuse, specular=spec, device=dev_index)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+
+    m = measure_scene(args, torch, dist, ctx, args.scene, rank, world, dev, stream)
+    key = profile_key(n, w, h, args.scene, args.gbuffer, args.n_diffuse, spec, args.variant, world)
+    rec, reason = load_profile(args.profile_json, key)
+    roof = roofline(rec, reason, m["k4_kernel_ms_avg"], m["local_texels"], m["local_valid"], args.profile_json, key)
 
     result = None
     if rank == 0:
         result = {
-            "metric": "Mcone-steps/s at 256^3 grid, 1080p, 9 diffuse + 1 spec cone; 1/2/4/8 GPUs",
-            "value": round(value, 2),
+            "metric": METRIC,
+            "value": round(m["value"], 2),
             "unit": "Mcone-steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": round(m["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -286,39 +522,40 @@ def main():
                             f"{args.n_diffuse} diffuse + {1 if spec else 0} specular cones",
                 "grid": n, "width": w, "height": h, "scene": args.scene, "gbuffer": args.gbuffer,
                 "n_diffuse": args.n_diffuse, "specular": spec, "parallelism": f"screen-tiles x{world}",
-                "variant": args.variant,
+                "exchange": args.exchange if world > 1 else None, "variant": args.variant,
             },
-            "frame_cone_steps": frame_steps,
-            "valid_px": frame_valid,
-            "k4_kernel_ms_avg": round(k4_avg_ms, 4),
-            "k4_kernel_ms_median": round(k4_med_ms, 4),
-            "k1_voxelize_ms": round(k1_ms, 3),
-            "k2_inject_ms": round(k2_ms, 3),
-            "k3_mips_ms": round(k3_ms, 3),
-            "grid_bcast_ms": round(bcast_ms, 3),
-            # a frame whose light changes: inject + mips + trace; at N > 1 the level-0 grid
-            # either comes from rank 0 by broadcast or every rank injects it itself
-            # (report the cheaper, keep the broadcast path); both are listed
-            "frame_relight_ms": round(min(k2_ms + bcast_ms, k2_rep_ms) + k3_ms + ms_per_step, 3),
-            "frame_relight_bcast_ms": round(k2_ms + bcast_ms + k3_ms + ms_per_step, 3),
-            "frame_relight_replicated_ms": round(k2_rep_ms + k3_ms + ms_per_step, 3),
-            "replicated_k2_equals_bcast": k2_rep_match,
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": bytes_launch,
-                "texel_fetches_per_launch": local_texels,
-            },
-            "cpu_baseline": None,
         }
+        for k_ in ("frame_cone_steps", "valid_px"):
+            result[k_] = m[k_]
+        result["k4_kernel_ms_avg"] = round(m["k4_kernel_ms_avg"], 4)
+        result["k4_kernel_ms_median"] = round(m["k4_kernel_ms_median"], 4)
+        for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
+                   "frame_relight_bcast_ms", "frame_relight_replicated_ms", "replicated_k2_equals_bcast",
+                   "trace_ms_max_rank", "gather_ms", "allgather_ms"):
+            if k_ in m:
+                result[k_] = m[k_]
+        result["roofline"] = roof
+        result["cpu_baseline"] = None
         if world == 1 and not args.no_cpu_baseline:
-            host = tuple(t_.cpu().numpy() for t_ in gb)
-            result["cpu_baseline"] = cpu_baseline(ctx, n, g0, E, host, eye, args.n_diffuse, spec,
-                                                  steps_px.cpu().numpy().astype(np.uint32), args.cpu_seconds)
+            host = tuple(t_.cpu().numpy() for t_ in m["_gb"])
+            result["cpu_baseline"] = cpu_baseline(ctx, n, g0, E, host, m["_eye"], args.n_diffuse, spec,
+                                                  m["_steps_px"].cpu().numpy().astype(np.uint32), args.cpu_seconds)
+    del m
+    torch.cuda.empty_cache()
+    sec = (args.secondary or "").strip()
+    if sec and sec != "none" and sec != args.scene:
+        # the same size on a non-flat scene (varied normals: fewer combined-face bricks)
+        s2 = measure_scene(args, torch, dist, ctx, sec, rank, world, dev, stream)
+        if rank == 0:
+            result["secondary"] = {
+                "scene": sec + STAND_IN.get(sec, ""), "value": round(s2["value"], 2), "unit": "Mcone-steps/s",
+                "ms_per_step": round(s2["ms_per_step"], 4), "k4_kernel_ms_avg": round(s2["k4_kernel_ms_avg"], 4),
+                "frame_cone_steps": s2["frame_cone_steps"], "valid_px": s2["valid_px"],
+                "k1_voxelize_ms": s2["k1_voxelize_ms"],
+            }
+            if "trace_ms_max_rank" in s2:
+                result["secondary"]["trace_ms_max_rank"] = s2["trace_ms_max_rank"]
+        del s2
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -173,6 +173,38 @@ vct_status vct_untile_device(vct_ctx* ctx, const float* gathered4, uint32_t widt
 vct_status vct_untile_planes_device(vct_ctx* ctx, const float* gathered4, uint32_t planes, uint32_t width,
                                     uint32_t height, uint32_t world, float* const* frames4);
 
+/* Packed form: rank r contributed exactly its own tiles, [planes][tiles(r)][64*64][4],
+ * at tile offset planes * vct_tile_offset(w,h,r,world) of gathered4 (no padding;
+ * the gather-to-one-rank layout of vct_comm_trace_frame and vct.multi). */
+vct_status vct_untile_planes_packed_device(vct_ctx* ctx, const float* gathered4, uint32_t planes, uint32_t width,
+                                           uint32_t height, uint32_t world, float* const* frames4);
+/* Tiles of ranks 0..rank-1 (= rank * q + min(rank, T mod world), T tiles, q = T / world). */
+uint32_t   vct_tile_offset(uint32_t width, uint32_t height, uint32_t rank, uint32_t world);
+
+/* ---- one process per GPU over RCCL -------------------------
+ * For a C/C++ host without torch (the reference engine, engine.cpp:140-157,
+ * started once per GPU).  Rank 0 calls vct_comm_get_id and hands the id to the
+ * other processes out of band; every rank calls vct_comm_init on its own
+ * vct_create context (not a vct_create_multi one).  Calls are collective and
+ * queued on the ctx stream. */
+typedef struct vct_comm_id { char internal[128]; } vct_comm_id;   /* = ncclUniqueId */
+#define VCT_ALL_RANKS (-1)
+vct_status vct_comm_get_id(vct_comm_id* out);
+vct_status vct_comm_init(vct_ctx* ctx, const vct_comm_id* id, uint32_t nranks, uint32_t rank);
+vct_status vct_comm_rank(const vct_ctx* ctx, uint32_t* rank, uint32_t* nranks);
+/* ncclBroadcast of the level-0 radiance grid from `root` (after its K2); every
+ * rank then runs vct_build_mips itself (the replicated mip pyramid). */
+vct_status vct_comm_broadcast_level0(vct_ctx* ctx, uint32_t root);
+/* One frame: trace this rank's tiles (tile t -> rank t % nranks; the tile_*
+ * fields of args must be 0), then assemble the whole [h][w][4] diffuse / spec
+ * frame into args->diffuse4 / spec4 on `root` only (the other ranks send their
+ * tiles there: ncclSend / ncclRecv, each rank moves only its own tiles), or on
+ * every rank for root = VCT_ALL_RANKS (one ncclAllGather).  Output pointers of
+ * non-receiving ranks are not written.  Counters count this rank's tiles. */
+vct_status vct_comm_trace_frame(vct_ctx* ctx, const vct_trace_args* args, int32_t root);
+/* Releases the communicator (vct_destroy also does). */
+vct_status vct_comm_destroy(vct_ctx* ctx);
+
 /* ---- G-buffer (input producer) -----------------------
  * Ray-casts the triangles of the last vct_voxelize call through `cam` into a
  * device G-buffer (pos4.w = 1 on hit, 0 on background).  Normals are the face

@@ -40,6 +40,7 @@ struct vct_ctx {
     float* tri;                     /* [n_tri][4][4]: v0, e1, e2, kd (as the HIP mesh records) */
     uint32_t n_tri;
     int voxelized, injected, mipped;
+    int comm;               /* vct_comm_init was called (one rank) */
     char err[256];
 };
 
@@ -159,7 +160,7 @@ static vct_status voxelize_common(vct_ctx* c, const void* verts, uint32_t stride
                              n_mat, c->sums, c->counts) != 0)
         bad = 1;
     vo_resolve(c->n, c->sums, c->counts, c->albedo_occ, c->normal);
-    c->voxelized = 1;
+    c->voxelized = !bad;     /* a partial grid (bad indices) is refused by inject / mips / trace */
     c->injected = c->mipped = 0;
     if (bad) return fail(c, VCT_EINVAL, "vertex or material index out of range");
     return VCT_OK;
@@ -284,22 +285,35 @@ vct_status vct_trace(vct_ctx* c, const float* pos4, const float* nrm4, const flo
     return VCT_OK;
 }
 
-static void untile(const float* g, uint32_t planes, uint32_t w, uint32_t h, uint32_t world, float* const* frames) {
+uint32_t vct_tile_offset(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
+    if (world == 0) world = 1;
+    if (rank >= world) return 0;
+    const uint32_t total = ((w + VCT_TILE - 1) / VCT_TILE) * ((h + VCT_TILE - 1) / VCT_TILE);
+    const uint32_t q = total / world, rem = total % world;
+    return rank * q + (rank < rem ? rank : rem);
+}
+
+/* packed: rank r's [planes][tiles(r)] block at tile offset planes * vct_tile_offset(r) */
+static void untile(const float* g, uint32_t planes, uint32_t w, uint32_t h, uint32_t world, float* const* frames,
+                   int packed) {
     const uint32_t tx = (w + VCT_TILE - 1) / VCT_TILE;
     const uint32_t maxt = vct_tiles_for_rank(w, h, 0, world);
     for (uint32_t p = 0; p < planes; ++p)
         for (uint32_t y = 0; y < h; ++y)
             for (uint32_t x = 0; x < w; ++x) {
                 const uint32_t t = (y / VCT_TILE) * tx + x / VCT_TILE, rank = t % world, lt = t / world;
-                const size_t src = (((size_t)rank * planes + p) * maxt + lt) * (VCT_TILE * VCT_TILE) +
-                                   (size_t)(y % VCT_TILE) * VCT_TILE + (x % VCT_TILE);
+                const size_t tile0 = packed ? (size_t)planes * vct_tile_offset(w, h, rank, world) +
+                                                  (size_t)p * vct_tiles_for_rank(w, h, rank, world)
+                                            : ((size_t)rank * planes + p) * maxt;
+                const size_t src = (tile0 + lt) * (VCT_TILE * VCT_TILE) + (size_t)(y % VCT_TILE) * VCT_TILE +
+                                   (x % VCT_TILE);
                 memcpy(frames[p] + 4 * ((size_t)y * w + x), g + 4 * src, 16);
             }
 }
 
 vct_status vct_untile_device(vct_ctx* c, const float* g, uint32_t w, uint32_t h, uint32_t world, float* frame4) {
     if (!c || !g || !frame4 || w == 0 || h == 0) return VCT_EINVAL;
-    untile(g, 1, w, h, world ? world : 1, &frame4);
+    untile(g, 1, w, h, world ? world : 1, &frame4, 0);
     return VCT_OK;
 }
 
@@ -308,7 +322,61 @@ vct_status vct_untile_planes_device(vct_ctx* c, const float* g, uint32_t planes,
     if (!c || !g || !frames4 || w == 0 || h == 0 || planes == 0 || planes > 4) return VCT_EINVAL;
     for (uint32_t p = 0; p < planes; ++p)
         if (!frames4[p]) return VCT_EINVAL;
-    untile(g, planes, w, h, world ? world : 1, frames4);
+    untile(g, planes, w, h, world ? world : 1, frames4, 0);
+    return VCT_OK;
+}
+
+vct_status vct_untile_planes_packed_device(vct_ctx* c, const float* g, uint32_t planes, uint32_t w, uint32_t h,
+                                           uint32_t world, float* const* frames4) {
+    if (!c || !g || !frames4 || w == 0 || h == 0 || planes == 0 || planes > 4) return VCT_EINVAL;
+    for (uint32_t p = 0; p < planes; ++p)
+        if (!frames4[p]) return VCT_EINVAL;
+    untile(g, planes, w, h, world ? world : 1, frames4, 1);
+    return VCT_OK;
+}
+
+/* ---- RCCL exchange: the CPU backend has no communicator; a one-rank "group"
+ * (nranks = 1) is accepted so a host's call sequence runs unchanged ------------ */
+vct_status vct_comm_get_id(vct_comm_id* out) {
+    if (!out) return VCT_EINVAL;
+    memset(out, 0, sizeof *out);
+    return VCT_OK;
+}
+
+vct_status vct_comm_init(vct_ctx* c, const vct_comm_id* id, uint32_t nranks, uint32_t rank) {
+    if (!c || !id || nranks == 0 || rank >= nranks) return VCT_EINVAL;
+    if (nranks != 1) return fail(c, VCT_ECOMM, "CPU backend: no RCCL, one rank only");
+    c->comm = 1;
+    return VCT_OK;
+}
+
+vct_status vct_comm_rank(const vct_ctx* c, uint32_t* rank, uint32_t* nranks) {
+    if (!c) return VCT_EINVAL;
+    if (rank) *rank = 0;
+    if (nranks) *nranks = 1;
+    return VCT_OK;
+}
+
+vct_status vct_comm_broadcast_level0(vct_ctx* c, uint32_t root) {
+    if (!c) return VCT_EINVAL;
+    if (!c->comm) return fail(c, VCT_ESTATE, "broadcast_level0 before comm_init");
+    if (root != 0) return fail(c, VCT_EINVAL, "broadcast_level0: root out of range");
+    if (!c->injected) return fail(c, VCT_ESTATE, "broadcast_level0: root has no level 0 (inject first)");
+    c->mipped = 0;
+    return VCT_OK;
+}
+
+vct_status vct_comm_trace_frame(vct_ctx* c, const vct_trace_args* a, int32_t root) {
+    if (!c || !a) return VCT_EINVAL;
+    if (!c->comm) return fail(c, VCT_ESTATE, "trace_frame before comm_init");
+    if (root != VCT_ALL_RANKS && root != 0) return fail(c, VCT_EINVAL, "trace_frame: root out of range");
+    if (a->tile_world > 1 || a->tile_compact) return fail(c, VCT_EINVAL, "trace_frame sets the tiling itself");
+    return vct_trace_device(c, a);
+}
+
+vct_status vct_comm_destroy(vct_ctx* c) {
+    if (!c) return VCT_EINVAL;
+    c->comm = 0;
     return VCT_OK;
 }
 

@@ -185,3 +185,117 @@ def test_multi_device_context_cpu(cpu_lib, oracle_mod):
     assert cpu_lib.vct_trace_device(one.h, C.byref(args)) == 0
     multi.close()
     one.close()
+
+
+def test_partial_grid_after_bad_indices_is_refused(cpu_lib):
+    """A voxelization that fails on out-of-range indices leaves no usable grid:
+    inject after it is VCT_ESTATE (the HIP library's rule too, test_parity_gpu)."""
+    from vct import Context, VctError, scenes
+    g0, E = scenes.grid_for_unit_box(16)
+    ctx = Context(16, g0, E, lib=cpu_lib)
+    v = np.zeros((3, 14), np.float32)
+    ctx.voxelize(v, np.array([0, 1, 2], np.uint32))
+    with pytest.raises(VctError, match="EINVAL"):
+        ctx.voxelize(v, np.array([0, 1, 5], np.uint32))
+    with pytest.raises(VctError, match="ESTATE"):
+        ctx.inject_directional((0, 1, 0))
+    ctx.voxelize(v, np.array([0, 1, 2], np.uint32))      # a good call restores the state
+    ctx.inject_directional((0, 1, 0))
+
+
+def test_host_argument_checks(cpu_lib):
+    """Python-side length / shape contracts of vct_voxelize (tri_material has n_idx / 3
+    entries, kd4 is [materials, 4]) are enforced before the C call."""
+    from vct import Context, VctError, scenes
+    g0, E = scenes.grid_for_unit_box(16)
+    ctx = Context(16, g0, E, lib=cpu_lib)
+    v = np.zeros((6, 14), np.float32)
+    idx = np.arange(6, dtype=np.uint32)
+    with pytest.raises(VctError, match="EINVAL.*tri_material"):
+        ctx.voxelize(v, idx, np.zeros(1, np.uint32), np.ones((1, 4), np.float32))
+    with pytest.raises(VctError, match="EINVAL.*kd4"):
+        ctx.voxelize(v, idx, np.zeros(2, np.uint32), np.ones(4, np.float32))
+    with pytest.raises(VctError, match="EINVAL.*multiple of 3"):
+        ctx.voxelize(v, idx[:4])
+    ctx.voxelize(v, idx, np.zeros(2, np.uint32), np.ones((1, 4), np.float32))
+
+
+class _FakeDeviceTensor:
+    """Just enough of a torch CUDA tensor for Context._dev's checks."""
+
+    def __init__(self, numel, dtype="torch.float32", index=0, contiguous=True, cuda=True, shape=None):
+        self.is_cuda = cuda
+        self.shape = shape or (numel,)
+        self.dtype = dtype
+        self._n, self._c = numel, contiguous
+        self.device = type("D", (), {"index": index, "__str__": lambda s: f"cuda:{index}"})()
+
+    def is_contiguous(self):
+        return self._c
+
+    def dim(self):
+        return len(self.shape)
+
+    def numel(self):
+        return self._n
+
+    def data_ptr(self):
+        return 0x1000
+
+
+def test_device_pointer_checks(cpu_lib):
+    """Context._dev refuses host tensors, the wrong device / dtype, non-contiguous and
+    undersized buffers before a pointer reaches the C-ABI (a host pointer or a short
+    output would fault or overrun the GPU); 64-bit indices are refused for K1."""
+    import torch
+    from vct import Context, VctError, scenes
+    g0, E = scenes.grid_for_unit_box(16)
+    ctx = Context(16, g0, E, lib=cpu_lib, device=0)
+    F = _FakeDeviceTensor
+    assert ctx._dev(F(64), "x", min_numel=64) == 0x1000
+    assert ctx._dev(None, "x") is None and ctx._dev(1234, "x") == 1234
+    with pytest.raises(VctError, match="EINVAL.*device .cuda. tensor"):
+        ctx._dev(torch.zeros(64), "x")
+    with pytest.raises(VctError, match="EINVAL.*context on device 0"):
+        ctx._dev(F(64, index=1), "x")
+    with pytest.raises(VctError, match="EINVAL.*dtype"):
+        ctx._dev(F(64, dtype="torch.float64"), "x")
+    with pytest.raises(VctError, match="EINVAL.*contiguous"):
+        ctx._dev(F(64, contiguous=False), "x")
+    with pytest.raises(VctError, match="EINVAL.*at least 65"):
+        ctx._dev(F(64), "x", min_numel=65)
+    # trace_device sizes every buffer from the frame (compact: the rank's tiles)
+    w, h = 100, 70
+    gb = [F(4 * w * h) for _ in range(3)]
+    with pytest.raises(VctError, match="EINVAL.*diffuse4"):
+        ctx.trace_device(*gb, w, h, (0, 0, 3), F(4 * w * h - 1), F(4 * w * h))
+    with pytest.raises(VctError, match="EINVAL.*steps_px.*dtype"):
+        ctx.trace_device(*gb, w, h, (0, 0, 3), F(4 * w * h), F(4 * w * h), steps_px=F(w * h))
+    with pytest.raises(VctError, match="EINVAL.*diffuse4"):
+        ctx.trace_device(*gb, w, h, (0, 0, 3), F(4 * 4096 - 4), F(4 * 4096), tile_rank=1, tile_world=2,
+                         tile_compact=True)
+    with pytest.raises(VctError, match="EINVAL.*64-bit"):
+        ctx.voxelize_device(F(14 * 3, shape=(3, 14)), F(3, dtype="torch.int64"))
+
+
+def test_comm_one_rank(cpu_lib):
+    """vct_comm_* on the CPU backend: a one-rank group runs a host's call sequence
+    unchanged (the HIP library runs the same sequence over RCCL on the GPU box)."""
+    from vct import VCT_ALL_RANKS, Context, VctError, scenes
+    from vct.camera import Camera
+    ctx, s, _, (g0, E) = _ctx(cpu_lib, n=16)
+    cid = Context.comm_get_id(cpu_lib)
+    assert len(cid) == 128
+    with pytest.raises(VctError, match="ECOMM"):
+        ctx.comm_init(cid, 2, 0)
+    ctx.comm_init(cid, 1, 0)
+    ctx.comm_broadcast_level0(0)
+    ctx.build_mips()
+    cam = Camera()
+    w, h = 48, 32
+    gb = scenes.raycast_numpy(s, cam, w, h)
+    d, sp = np.zeros((h, w, 4), np.float32), np.zeros((h, w, 4), np.float32)
+    ctx.comm_trace_frame(*[_ptr(b) for b in gb], w, h, cam.position, _ptr(d), _ptr(sp), root=VCT_ALL_RANKS)
+    ref = ctx.trace(*gb, cam.position)
+    assert np.array_equal(d, ref["diffuse"]) and np.array_equal(sp, ref["spec"])
+    ctx.comm_destroy()

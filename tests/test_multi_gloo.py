@@ -103,3 +103,110 @@ def test_tiles_for_rank_matches_c_abi():
     for (w, h, world) in [(1920, 1080, 1), (1920, 1080, 8), (3840, 2160, 3), (65, 65, 2), (10, 10, 7)]:
         for r in range(world):
             assert tiles_for_rank(w, h, r, world) == multi.tiles_for_rank(w, h, r, world)
+
+
+def _present_worker(rank, world, port, out_dir):
+    """The gather-to-the-presenting-rank flow: each rank sends exactly its own tiles
+    ([2][tiles(r)*64*64][4], no padding) to rank 0, which un-permutes the packed buffer."""
+    import sys
+    for p in (REPO, os.path.join(REPO, "voxel-based-global-illumination_amd")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle as O
+    from vct import multi, scenes
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 16
+    s, g0, E, cam, (pos, nrm, alb) = _setup(n)
+    h, w = pos.shape[:2]
+    v, i, m, k = s.arrays()
+    st = O.pipeline(n, g0, E, v, i, m, k, scenes.LIGHT_DIR)     # K1-K3 replicated on every rank
+    fi, ci = multi.compact_index(w, h, rank, world)
+    mine = np.zeros(h * w, bool)
+    mine[fi] = True
+    pos_l = pos.copy()
+    pos_l.reshape(-1, 4)[~mine, 3] = 0
+    res = O.trace(n, g0, E, st["r0"], st["pyr"], pos_l, nrm, alb, cam.position, threads=1)
+    nt = multi.tiles_for_rank(w, h, rank, world)
+    comp = np.zeros((2, nt * 4096, 4), np.float32)
+    comp[0, ci] = res["diffuse"].reshape(-1, 4)[fi]
+    comp[1, ci] = res["spec"].reshape(-1, 4)[fi]
+    _, _, total = multi.num_tiles(w, h)
+    if rank == 0:
+        packed = torch.zeros((2 * total * 4096, 4), dtype=torch.float32)
+        packed[: comp.size // 4] = torch.from_numpy(comp.reshape(-1, 4))
+        ops = []
+        for r in range(1, world):
+            off = 2 * multi.tile_offset(w, h, r, world) * 4096
+            ops.append(dist.P2POp(dist.irecv, packed[off:off + 2 * multi.tiles_for_rank(w, h, r, world) * 4096], r))
+        for wk in dist.batch_isend_irecv(ops):
+            wk.wait()
+        d, sp = multi.untile_packed(packed.numpy(), w, h, world, 2)
+        np.save(os.path.join(out_dir, "present.npy"), np.concatenate([d, sp], -1))
+    else:
+        for wk in dist.batch_isend_irecv([dist.P2POp(dist.isend, torch.from_numpy(comp.reshape(-1, 4)), 0)]):
+            wk.wait()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_present_gather_matches_single_rank(oracle_mod, tmp_path, world):
+    import torch.multiprocessing as mp
+    mp.spawn(_present_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    O = oracle_mod
+    from vct import scenes
+    n = 16
+    s, g0, E, cam, (pos, nrm, alb) = _setup(n)
+    v, i, m, k = s.arrays()
+    st = O.pipeline(n, g0, E, v, i, m, k, scenes.LIGHT_DIR)
+    ref = O.trace(n, g0, E, st["r0"], st["pyr"], pos, nrm, alb, cam.position)
+    assert np.array_equal(np.load(tmp_path / "present.npy"), np.concatenate([ref["diffuse"], ref["spec"]], -1))
+
+
+def _tracer_worker(rank, world, port, out_dir, mode, w, h):
+    import sys
+    for p in (REPO, os.path.join(REPO, "voxel-based-global-illumination_amd")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from vct.multi import FrameTracer, PatternContext
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = FrameTracer(PatternContext(torch), torch, dist, w, h, rank, world, torch.device("cpu"), mode=mode)
+    for _ in range(3):
+        tr.step((None, None, None), (0.0, 0.0, 3.0))
+    tr.drain()
+    if tr.holds_frame:
+        np.save(os.path.join(out_dir, f"t{rank}.npy"), np.concatenate([tr.diff.numpy(), tr.spec.numpy()], -1))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,world,w,h", [("present", 2, 150, 70), ("present", 3, 200, 130), ("allgather", 3, 130, 65),
+                                           ("present", 4, 64, 64)])
+def test_frame_tracer_exchange_modes(tmp_path, mode, world, w, h):
+    """vct.multi.FrameTracer's own exchange code (the one bench.py runs) in both modes:
+    present -> only rank 0 holds the frame; allgather -> every rank; frames exact.
+    (world 4 on a one-tile frame: ranks 1-3 own no tile and send nothing.)"""
+    import torch.multiprocessing as mp
+    mp.spawn(_tracer_worker, args=(world, _free_port(), str(tmp_path), mode, w, h), nprocs=world, join=True)
+    ref = np.arange(w * h, dtype=np.float32).reshape(h, w, 1).repeat(4, 2)
+    holders = [0] if mode == "present" else list(range(world))
+    for r in range(world):
+        f = tmp_path / f"t{r}.npy"
+        assert f.exists() == (r in holders)
+        if r in holders:
+            got = np.load(f)
+            assert np.array_equal(got[..., :4], ref) and np.array_equal(got[..., 4:], -ref)
+
+
+@pytest.mark.parametrize("w,h,world", [(1920, 1080, 8), (3840, 2160, 8), (150, 70, 3), (64, 64, 4)])
+def test_tile_offset_matches_c_abi(w, h, world):
+    from vct import multi, tile_offset
+    acc = 0
+    for r in range(world):
+        assert multi.tile_offset(w, h, r, world) == tile_offset(w, h, r, world) == acc
+        acc += multi.tiles_for_rank(w, h, r, world)
+    assert acc == multi.num_tiles(w, h)[2]

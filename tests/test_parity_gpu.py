@@ -243,9 +243,68 @@ def test_tiled_trace_equals_full_frame(gpu_ready, world):
     torch.cuda.synchronize()
     assert torch.equal(fd2, full_d) and torch.equal(fs2, full_s)
     # host mirror of the permutation agrees with the device one
-    from vct.multi import untile
+    from vct.multi import tile_offset, untile
     host = untile(g_d.cpu().numpy(), w, h, world)
     assert np.array_equal(host, full_d.cpu().numpy())
+    # packed layout (gather to the presenting rank): rank r's [2][tiles(r)] tiles at
+    # tile offset 2 * tile_offset(r), no padding, traced straight into its slice
+    T = tiles_for_rank(w, h, 0, 1)
+    packed = torch.zeros((2 * T * 4096, 4), device=dev)
+    for r in range(world):
+        nt, off = tiles_for_rank(w, h, r, world), 2 * tile_offset(w, h, r, world) * 4096
+        if nt:
+            sl = packed[off:off + 2 * nt * 4096].view(2, nt * 4096, 4)
+            ctx.trace_device(pos, nrm, alb, w, h, cam.position, sl[0], sl[1], tile_rank=r, tile_world=world,
+                             tile_compact=True)
+    fd3, fs3 = torch.zeros_like(fd), torch.zeros_like(fs)
+    ctx.untile_planes_device(packed, w, h, world, (fd3, fs3), packed=True)
+    torch.cuda.synchronize()
+    assert torch.equal(fd3, full_d) and torch.equal(fs3, full_s)
+    ctx.close()
+
+
+def test_comm_one_rank_rccl(gpu_ready):
+    """vct_comm_* through the HIP library over a one-rank RCCL communicator (the
+    one-GPU box cannot hold two RCCL ranks): broadcast of level 0 and the frame
+    assembled on the root (send/recv form) and on every rank (all-gather form)
+    equal the plain trace bit for bit."""
+    import torch
+    from vct import VCT_ALL_RANKS, Context, scenes
+    from vct.camera import Camera
+    ctx, s, arrs, (g0, E) = gpu_pipeline(32, "atrium")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.comm_init(Context.comm_get_id(), 1, 0)
+    ctx.comm_broadcast_level0(0)
+    ctx.build_mips()
+    w, h = 200, 130
+    cam = Camera()
+    dev = torch.device("cuda")
+    pos, nrm, alb = (torch.empty((h, w, 4), device=dev) for _ in range(3))
+    ctx.gbuffer_raycast_device(cam, w, h, scenes.ROUGHNESS, pos, nrm, alb)
+    full_d, full_s = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+    ctx.trace_device(pos, nrm, alb, w, h, cam.position, full_d, full_s)
+    for root in (0, VCT_ALL_RANKS):
+        d, sp = torch.zeros_like(full_d), torch.zeros_like(full_s)
+        ctx.comm_trace_frame(pos, nrm, alb, w, h, cam.position, d, sp, root=root)
+        torch.cuda.synchronize()
+        assert torch.equal(d, full_d) and torch.equal(sp, full_s), root
+    ctx.comm_destroy()
+    ctx.close()
+
+
+def test_partial_grid_refused_gpu(gpu_ready):
+    """After a voxelization with out-of-range indices the grid is partial: inject is
+    refused with VCT_ESTATE until a good voxelization."""
+    from vct import Context, VctError
+    ctx = Context(16, (0, 0, 0), 1.0)
+    v = np.zeros((3, 14), np.float32)
+    ctx.voxelize(v, np.array([0, 1, 2], np.uint32))
+    with pytest.raises(VctError, match="EINVAL"):
+        ctx.voxelize(v, np.array([0, 1, 5], np.uint32))
+    with pytest.raises(VctError, match="ESTATE"):
+        ctx.inject_directional((0, 1, 0))
+    ctx.voxelize(v, np.array([0, 1, 2], np.uint32))
+    ctx.inject_directional((0, 1, 0))
     ctx.close()
 
 
@@ -265,6 +324,7 @@ class _FakeGroup:
 
     def __init__(self, world):
         self.world, self.inputs, self.round = world, {}, [0] * world
+        self.sends, self.p2p_round = {}, {}
 
     def view(self, rank):
         g = self
@@ -285,16 +345,40 @@ class _FakeGroup:
                     done()
                     return None
                 return _FakeWork(done)
+
+            # point-to-point (the "present" exchange): a send is kept by reference and
+            # copied when the matching receive's work is waited on (same round per pair)
+            isend, irecv = "isend", "irecv"
+
+            class P2POp:
+                def __init__(self, op, tensor, peer):
+                    self.op, self.tensor, self.peer = op, tensor, peer
+
+            def batch_isend_irecv(self, ops):
+                works = []
+                for o in ops:
+                    src, dst = (rank, o.peer) if o.op == "isend" else (o.peer, rank)
+                    rd = g.p2p_round.get((src, dst, o.op), 0)
+                    g.p2p_round[(src, dst, o.op)] = rd + 1
+                    if o.op == "isend":
+                        g.sends[(rd, src, dst)] = o.tensor
+                        works.append(_FakeWork(lambda: None))
+                    else:
+                        works.append(_FakeWork(lambda t=o.tensor, k=(rd, src, dst): t.copy_(g.sends[k].view_as(t))))
+                return works
         return View()
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_frame_pipeline_equals_full_frames(gpu_ready, world):
+@pytest.mark.parametrize("world,mode", [(1, "present"), (2, "present"), (3, "present"), (2, "allgather"),
+                                        (3, "allgather")])
+def test_frame_pipeline_equals_full_frames(gpu_ready, world, mode):
     """FrameTracer (bench.py's per-rank driver): the pipelined step()/drain() loop
-    (all-gather of frame f overlapping the trace of frame f+1, two buffer sets,
-    one [diffuse | specular] gather, one two-plane untile) yields every frame
-    bit-identical to a single-rank trace of it.  Ranks are FrameTracers in one
-    process over a fake group; each frame uses a different eye (specular changes)."""
+    (the exchange of frame f overlapping the trace of frame f+1, two buffer sets,
+    [diffuse | specular] moved together, one two-plane untile) yields every frame
+    bit-identical to a single-rank trace of it, on rank 0 only ("present": send /
+    recv of each rank's own tiles, packed) or on every rank ("allgather").  Ranks
+    are FrameTracers in one process over a fake group; each frame uses a different
+    eye (specular changes)."""
     import torch
     from vct import scenes
     from vct.camera import Camera
@@ -313,7 +397,7 @@ def test_frame_pipeline_equals_full_frames(gpu_ready, world):
         ctx.trace_device(pos, nrm, alb, w, h, e, d, sp)
         refs.append((d, sp))
     grp = _FakeGroup(world)
-    tr = [FrameTracer(ctx, torch, grp.view(r), w, h, r, world, dev) for r in range(world)]
+    tr = [FrameTracer(ctx, torch, grp.view(r), w, h, r, world, dev, mode=mode) for r in range(world)]
     for f, e in enumerate(eyes):
         for t in tr:
             t.step((pos, nrm, alb), e)
@@ -322,12 +406,15 @@ def test_frame_pipeline_equals_full_frames(gpu_ready, world):
         if done >= 0:
             torch.cuda.synchronize()
             for t in tr:
-                assert torch.equal(t.diff, refs[done][0]) and torch.equal(t.spec, refs[done][1]), (f, t.rank)
+                if t.holds_frame:
+                    assert torch.equal(t.diff, refs[done][0]) and torch.equal(t.spec, refs[done][1]), (f, t.rank)
     for t in tr:
         t.drain()
     torch.cuda.synchronize()
+    assert sum(t.holds_frame for t in tr) == (1 if mode == "present" else world)
     for t in tr:
-        assert torch.equal(t.diff, refs[-1][0]) and torch.equal(t.spec, refs[-1][1])
+        if t.holds_frame:
+            assert torch.equal(t.diff, refs[-1][0]) and torch.equal(t.spec, refs[-1][1])
     ctx.close()
 
 

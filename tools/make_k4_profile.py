@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Per-launch rocprofv3 record of bench.py's timed K4 form (the roofline input).
+
+    make_k4_profile.py <prof_dir> --tag T [bench args]   -> gpurun_out/k4_counters_T.json
+    make_k4_profile.py --merge gpurun_out/k4_counters_T.json [...]   -> profiles/k4_counters.json
+
+The timed form is the k4_trace instantiation compiled without the counters
+(last template argument `false`); every PMC value is the mean over its
+dispatches.  HBM traffic = (2 FETCH_SIZE + WRITE_SIZE) KiB x 1024 per launch:
+on gfx950 FETCH_SIZE counts half the bytes of wide reads (MI355X_MICROARCH.md
+'HBM').  The record carries the sha256 of the libvct_hip.so it was measured on;
+bench.py uses it only for that build.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+TIMED = re.compile(r"k4_trace<[^>]*, false>\(")
+
+
+def per_kernel(d):
+    vals, durs = {}, []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if TIMED.search(r["Kernel_Name"]):
+                    vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if TIMED.search(r["Kernel_Name"]):
+                    durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    out = {k: sum(v) / len(v) for k, v in sorted(vals.items())}
+    out["dispatches"] = len(durs)
+    out["duration_ms"] = sum(durs) / len(durs) / 1e6 if durs else None
+    return out
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--merge":
+        path = os.path.join(REPO, "profiles", "k4_counters.json")
+        db = json.load(open(path)) if os.path.exists(path) else {}
+        for f in sys.argv[2:]:
+            db.update(json.load(open(f)))
+        with open(path, "w") as fh:
+            json.dump(db, fh, indent=1, sort_keys=True)
+        print(f"{path}: {len(db)} entries")
+        return
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir")
+    ap.add_argument("--tag", required=True)
+    a, rest = ap.parse_known_args()
+    import bench
+    sys.argv = ["bench.py"] + rest
+    b = bench.parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    key = bench.profile_key(b.n, b.width, b.height, b.scene, b.gbuffer, b.n_diffuse, not b.no_spec, b.variant, world)
+    s = per_kernel(a.prof_dir)
+    rec = dict(s)
+    rec.update({
+        "lib_sha256": bench.lib_sha256(),
+        "source": os.path.relpath(a.prof_dir, REPO),
+        "tag": a.tag,
+        "hbm_bytes_per_launch": int(2 * s["FETCH_SIZE"] * 1024 + s["WRITE_SIZE"] * 1024),
+        "l2_hit_rate": s["TCC_HIT_sum"] / max(1.0, s["TCC_HIT_sum"] + s["TCC_MISS_sum"]),
+        "correction": "hbm = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halves wide reads)",
+    })
+    out = {key: rec}
+    path = os.path.join(REPO, "gpurun_out", f"k4_counters_{a.tag}.json")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()

@@ -208,6 +208,7 @@ uint32_t vct_num_devices(const vct_ctx* c) { return c ? 1u + (uint32_t)c->peers.
 
 void vct_destroy(vct_ctx* c) {
     if (!c) return;
+    (void)vct_comm_destroy(c);
     for (vct_ctx* p : c->peers) vct_destroy(p);
     c->peers.clear();
     (void)hipSetDevice(c->device);
@@ -286,7 +287,8 @@ static vct_status voxelize_dev(vct_ctx* c, const void* dv, uint32_t stride, uint
     int herr = 0;
     VCT_HIP(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, c->stream), "download err");
     VCT_HIP(hipStreamSynchronize(c->stream), "voxelize sync");
-    c->grid.voxelized = true;
+    // a grid from out-of-range indices is partial: inject / mips / trace refuse it (VCT_ESTATE)
+    c->grid.voxelized = herr == 0;
     c->grid.injected = c->grid.mipped = false;
     if (herr) return fail(c, VCT_EINVAL, "vertex or material index out of range");
     return VCT_OK;
@@ -537,6 +539,29 @@ vct_status vct_untile_planes_device(vct_ctx* c, const float* gathered4, uint32_t
     if (st != VCT_OK) return st;
     VCT_HIP(launch_untile(c, (const float4*)gathered4, planes, w, h, world, f), "untile planes");
     return VCT_OK;
+}
+
+vct_status vct_untile_planes_packed_device(vct_ctx* c, const float* gathered4, uint32_t planes, uint32_t w,
+                                           uint32_t h, uint32_t world, float* const* frames4) {
+    if (!c || !gathered4 || !frames4 || w == 0 || h == 0 || planes == 0 || planes > (uint32_t)kMaxUntilePlanes)
+        return VCT_EINVAL;
+    float4* f[kMaxUntilePlanes] = {};
+    for (uint32_t p = 0; p < planes; ++p) {
+        if (!frames4[p]) return VCT_EINVAL;
+        f[p] = (float4*)frames4[p];
+    }
+    vct_status st = use_device(c);
+    if (st != VCT_OK) return st;
+    VCT_HIP(launch_untile(c, (const float4*)gathered4, planes, w, h, world, f, true), "untile planes packed");
+    return VCT_OK;
+}
+
+uint32_t vct_tile_offset(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
+    if (world == 0) world = 1;
+    if (rank >= world) return 0;
+    const uint32_t total = ((w + VCT_TILE - 1) / VCT_TILE) * ((h + VCT_TILE - 1) / VCT_TILE);
+    const uint32_t q = total / world, rem = total % world;
+    return rank * q + (rank < rem ? rank : rem);
 }
 
 vct_status vct_gbuffer_raycast_device(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h,

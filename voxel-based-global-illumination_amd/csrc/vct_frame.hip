@@ -13,10 +13,14 @@ namespace {
 // [world][planes][max_tiles][64*64] rank-compact tiles -> planes x [h][w] frame
 // (blockIdx.z = plane; each rank's planes are contiguous, as one all-gather of
 // the rank's [planes][max_tiles*64*64] buffer lays them out)
+// packed = 1: rank r's [planes][tiles(r)][64*64] block starts at tile offset
+// planes * prefix(r) with no padding (the gather-to-the-presenting-rank layout:
+// every rank sends exactly its own tiles); tiles(r) = q + (r < rem), prefix(r) =
+// r q + min(r, rem) for T = q world + rem tiles.
 struct UntileK {
     const float4* g;
     float4* frame[kMaxUntilePlanes];
-    int w, h, world, tiles_x, max_tiles, planes;
+    int w, h, world, tiles_x, max_tiles, planes, packed, q, rem;
 };
 
 __global__ void __launch_bounds__(256) k_untile(const UntileK k) {
@@ -26,8 +30,14 @@ __global__ void __launch_bounds__(256) k_untile(const UntileK k) {
     if (x >= k.w || y >= k.h) return;
     const int t = (y / VCT_TILE) * k.tiles_x + (x / VCT_TILE);
     const int rank = t % k.world, lt = t / k.world;
-    const size_t src = (((size_t)rank * k.planes + p) * k.max_tiles + lt) * (VCT_TILE * VCT_TILE) +
-                       (size_t)(y % VCT_TILE) * VCT_TILE + (x % VCT_TILE);
+    size_t tile0;   // first tile of (rank, plane) in the gathered buffer
+    if (k.packed) {
+        const int nt = k.q + (rank < k.rem ? 1 : 0), pre = rank * k.q + min(rank, k.rem);
+        tile0 = (size_t)k.planes * pre + (size_t)p * nt;
+    } else {
+        tile0 = ((size_t)rank * k.planes + p) * k.max_tiles;
+    }
+    const size_t src = (tile0 + lt) * (VCT_TILE * VCT_TILE) + (size_t)(y % VCT_TILE) * VCT_TILE + (x % VCT_TILE);
     k.frame[p][(size_t)y * k.w + x] = k.g[src];
 }
 
@@ -321,9 +331,13 @@ uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
 }
 
 hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t planes, uint32_t w, uint32_t h,
-                         uint32_t world, float4* const* frames) {
+                         uint32_t world, float4* const* frames, bool packed) {
     if (world == 0) world = 1;
     UntileK k{};
+    const uint32_t total = ((w + VCT_TILE - 1) / VCT_TILE) * ((h + VCT_TILE - 1) / VCT_TILE);
+    k.packed = packed ? 1 : 0;
+    k.q = (int)(total / world);
+    k.rem = (int)(total % world);
     k.g = gathered;
     for (uint32_t p = 0; p < planes; ++p) k.frame[p] = frames[p];
     k.w = (int)w; k.h = (int)h; k.world = (int)world; k.planes = (int)planes;

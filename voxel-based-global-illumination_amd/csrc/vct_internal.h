@@ -65,6 +65,8 @@ struct vct_ctx {
     // further device (ranks 1..n-1); empty for a single-device context
     std::vector<vct_ctx*> peers;
     hipEvent_t ev = nullptr;            // cross-device ordering of the multi-device calls
+    void* comm = nullptr;               // RCCL communicator of vct_comm_init (ncclComm_t), one process per GPU
+    int comm_rank = 0, comm_size = 1;
     bool own_stream = false;            // stream created by vct_create_multi (destroyed with the ctx)
     std::string err;
 };
@@ -82,7 +84,7 @@ hipError_t launch_mips(vct_ctx* c);
 // K4
 hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a);
 hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t planes, uint32_t w, uint32_t h,
-                         uint32_t world, float4* const* frames);
+                         uint32_t world, float4* const* frames, bool packed = false);
 // composite + present (row f3)
 hipError_t launch_composite(vct_ctx* c, const float4* pos, const float4* nrm, const float4* alb,
                             const float4* diff, const float4* spec, uint32_t w, uint32_t h, const float l[3],

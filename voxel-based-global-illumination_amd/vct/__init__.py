@@ -11,8 +11,11 @@ surface:
 * :mod:`vct.scenes` builds synthetic scenes in the reference ``Vertex`` layout
   (include/stdafx.h:36-42, 56-byte records) with per-material Kd
   (scene/material.h:10), and the G-buffers of SURVEY.md 8d;
-* :mod:`vct.renderer` is the ``Renderer`` / ``ConeTraceRenderer`` pair and the
-  name-keyed registry (core/assets.h:17-20, assets.cpp:44, engine.cpp:151).
+* :mod:`vct.multi` splits the cone trace over ranks (screen tiles, RCCL
+  broadcast of level 0, gather of the frame).
+The ``Renderer`` / ``ConeTraceRenderer`` slot and the name-keyed registry
+(core/assets.h:17-20, assets.cpp:44, engine.cpp:151) are in the C++ host
+(``host/renderer.h``, ``host/assets.h``).
 
 Host arrays are numpy; device arrays are torch tensors (torch is used only for
 device memory, streams and torch.distributed).
@@ -24,9 +27,10 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import VctCamera, VctConfig, VctTraceArgs
+from ._lib import VCT_ALL_RANKS, VctCamera, VctCommId, VctConfig, VctTraceArgs
 
-__all__ = ["Context", "VctError", "VctConfig", "VctCamera", "tiles_for_rank", "VERTEX_FLOATS"]
+__all__ = ["Context", "VctError", "VctConfig", "VctCamera", "tiles_for_rank", "tile_offset", "VERTEX_FLOATS",
+           "VCT_ALL_RANKS"]
 
 VERTEX_FLOATS = 14          # reference Vertex: Position, Normal, TexCoords, Tangent, Bitangent
 VERTEX_STRIDE = VERTEX_FLOATS * 4
@@ -48,6 +52,16 @@ def _f3(v):
 
 def tiles_for_rank(w: int, h: int, rank: int, world: int) -> int:
     return int(_lib.load().vct_tiles_for_rank(w, h, rank, world))
+
+
+def tile_offset(w: int, h: int, rank: int, world: int) -> int:
+    return int(_lib.load().vct_tile_offset(w, h, rank, world))
+
+
+_EINVAL = 1
+_F32 = ("torch.float32",)
+_I32 = ("torch.int32", "torch.uint32")
+_I64 = ("torch.int64", "torch.uint64")
 
 
 class Context:
@@ -76,6 +90,7 @@ class Context:
         if st != 0:
             raise VctError(st, "vct_create failed (is a HIP device visible?)")
         self.num_devices = int(self.lib.vct_num_devices(h))
+        self.device = int(device)
         self.h = h
         self.n = n
         self.aniso = aniso
@@ -107,6 +122,26 @@ class Context:
             err = self.lib.vct_last_error(self.h)
             raise VctError(st, f"{what}: {err.decode() if err else ''}")
 
+    def _dev(self, t, name: str, dtypes=_F32, min_numel: int = 0):
+        """Device pointer of a torch tensor after checking that the C-ABI may use it:
+        a CUDA tensor on this context's device, of an accepted dtype, contiguous,
+        with at least `min_numel` elements (an undersized output would be written
+        out of bounds, a host tensor would fault the GPU).  None stays None; a raw
+        int is taken as a device pointer the caller vouches for."""
+        if t is None or isinstance(t, int):
+            return t
+        if not getattr(t, "is_cuda", False):
+            raise VctError(_EINVAL, f"{name}: expected a device (cuda) tensor, got {getattr(t, 'device', type(t))}")
+        if self.device >= 0 and t.device.index != self.device:
+            raise VctError(_EINVAL, f"{name}: tensor on {t.device}, context on device {self.device}")
+        if str(t.dtype) not in dtypes:
+            raise VctError(_EINVAL, f"{name}: dtype {t.dtype}, expected one of {', '.join(dtypes)}")
+        if not t.is_contiguous():
+            raise VctError(_EINVAL, f"{name}: tensor is not contiguous")
+        if t.numel() < min_numel:
+            raise VctError(_EINVAL, f"{name}: {t.numel()} elements, needs at least {min_numel}")
+        return t.data_ptr()
+
     def set_stream(self, stream_ptr: int | None):
         self._check(self.lib.vct_set_stream(self.h, C.c_void_p(stream_ptr or 0)), "set_stream")
 
@@ -129,8 +164,16 @@ class Context:
         assert verts.ndim == 2 and verts.shape[1] >= 3
         stride = verts.shape[1] * 4
         idx = np.ascontiguousarray(idx, dtype=np.uint32).reshape(-1)
-        mat = None if tri_material is None else np.ascontiguousarray(tri_material, dtype=np.uint32)
-        kd = None if kd4 is None else np.ascontiguousarray(kd4, dtype=np.float32).reshape(-1, 4)
+        mat = None if tri_material is None else np.ascontiguousarray(tri_material, dtype=np.uint32).reshape(-1)
+        kd = None if kd4 is None else np.ascontiguousarray(kd4, dtype=np.float32)
+        if idx.size % 3:
+            raise VctError(_EINVAL, f"voxelize: {idx.size} indices, not a multiple of 3")
+        if mat is not None and mat.size != idx.size // 3:
+            # vct_voxelize reads n_idx / 3 entries of tri_material
+            raise VctError(_EINVAL, f"voxelize: tri_material has {mat.size} entries for {idx.size // 3} triangles")
+        if kd is not None:
+            if kd.ndim != 2 or kd.shape[1] != 4:
+                raise VctError(_EINVAL, f"voxelize: kd4 must be [materials, 4], got {kd.shape}")
         st = self.lib.vct_voxelize(self.h, _fptr(verts), stride, verts.shape[0], _fptr(idx), idx.size,
                                    _fptr(mat) if mat is not None else None,
                                    _fptr(kd) if kd is not None else None,
@@ -141,11 +184,21 @@ class Context:
         """K1 on device-resident torch tensors: verts [V, F] float32 (F >= 3, the
         56-byte Vertex is F = 14), idx [3T] int32/uint32, tri_material [T] int32,
         kd4 [M, 4] float32."""
-        assert verts.dim() == 2 and verts.shape[1] >= 3 and verts.is_contiguous()
-        ptr = lambda t: None if t is None else t.data_ptr()
+        if verts.dim() != 2 or verts.shape[1] < 3:
+            raise VctError(_EINVAL, f"voxelize_device: verts must be [V, F >= 3], got {tuple(verts.shape)}")
+        if str(idx.dtype) in _I64:
+            # read as uint32 pairs, the triangles would silently collapse onto vertex 0
+            raise VctError(_EINVAL, "voxelize_device: idx must be int32 / uint32, not 64-bit")
+        n_idx = idx.numel()
+        if n_idx % 3:
+            raise VctError(_EINVAL, f"voxelize_device: {n_idx} indices, not a multiple of 3")
+        if kd4 is not None and (kd4.dim() != 2 or kd4.shape[1] != 4):
+            raise VctError(_EINVAL, f"voxelize_device: kd4 must be [materials, 4], got {tuple(kd4.shape)}")
         nm = 0 if kd4 is None else kd4.shape[0]
-        st = self.lib.vct_voxelize_device(self.h, ptr(verts), verts.shape[1] * 4, verts.shape[0], ptr(idx),
-                                          idx.numel(), ptr(tri_material), ptr(kd4), nm)
+        st = self.lib.vct_voxelize_device(
+            self.h, self._dev(verts, "verts"), verts.shape[1] * 4, verts.shape[0], self._dev(idx, "idx", _I32),
+            n_idx, self._dev(tri_material, "tri_material", _I32, n_idx // 3),
+            self._dev(kd4, "kd4"), nm)
         self._check(st, "voxelize_device")
 
     def inject_directional(self, dir_to_light, color=(1.0, 1.0, 1.0)):
@@ -177,52 +230,105 @@ class Context:
                      variant=0):
         """Device-resident trace; arguments are torch CUDA tensors (or raw int pointers)."""
         a = VctTraceArgs()
-        ptr = lambda t: None if t is None else (t if isinstance(t, int) else t.data_ptr())
-        a.pos4, a.nrm4, a.alb4 = ptr(pos4), ptr(nrm4), ptr(alb4)
+        px = width * height
+        out_px = tiles_for_rank(width, height, tile_rank, tile_world) * 64 * 64 if tile_compact else px
+        a.pos4 = self._dev(pos4, "pos4", _F32, 4 * px)
+        a.nrm4 = self._dev(nrm4, "nrm4", _F32, 4 * px)
+        a.alb4 = self._dev(alb4, "alb4", _F32, 4 * px)
         a.width, a.height = width, height
         a.eye = _f3(eye)
-        a.diffuse4, a.spec4 = ptr(diffuse4), ptr(spec4)
-        a.steps_px, a.cone_steps = ptr(steps_px), ptr(cone_steps)
-        a.texel_fetches = ptr(texel_fetches)
+        a.diffuse4 = self._dev(diffuse4, "diffuse4", _F32, 4 * out_px)
+        a.spec4 = self._dev(spec4, "spec4", _F32, 4 * out_px)
+        a.steps_px = self._dev(steps_px, "steps_px", _I32, px)
+        a.cone_steps = self._dev(cone_steps, "cone_steps", _I64, 1)
+        a.texel_fetches = self._dev(texel_fetches, "texel_fetches", _I64, 1)
         a.tile_rank, a.tile_world = tile_rank, tile_world
         a.tile_compact = 1 if tile_compact else 0
         a.variant = variant
         self._check(self.lib.vct_trace_device(self.h, C.byref(a)), "trace_device")
 
     def untile_device(self, gathered4, width, height, world, frame4):
-        ptr = lambda t: t if isinstance(t, int) else t.data_ptr()
-        self._check(self.lib.vct_untile_device(self.h, ptr(gathered4), width, height, world, ptr(frame4)),
+        g = self._dev(gathered4, "gathered4", _F32, max(world, 1) * tiles_for_rank(width, height, 0, world) * 4096 * 4)
+        self._check(self.lib.vct_untile_device(self.h, g, width, height, world,
+                                               self._dev(frame4, "frame4", _F32, width * height * 4)),
                     "untile_device")
 
-    def untile_planes_device(self, gathered4, width, height, world, frames4):
-        """gathered4: [world][planes][max_tiles*64*64][4]; frames4: sequence of [h][w][4] outputs."""
-        ptr = lambda t: t if isinstance(t, int) else t.data_ptr()
-        arr = (C.c_void_p * len(frames4))(*[ptr(f) for f in frames4])
-        self._check(self.lib.vct_untile_planes_device(self.h, ptr(gathered4), len(frames4), width, height, world,
-                                                      C.cast(arr, C.c_void_p)), "untile_planes_device")
+    def untile_planes_device(self, gathered4, width, height, world, frames4, packed=False):
+        """gathered4: [world][planes][max_tiles*64*64][4] (one all-gather of equal-size
+        rank buffers) or, packed, rank r's [planes][tiles(r)*64*64][4] at tile offset
+        planes * tile_offset(r) (the gather to one rank); frames4: [h][w][4] outputs."""
+        planes = len(frames4)
+        need = (planes * tiles_for_rank(width, height, 0, 1) if packed
+                else max(world, 1) * planes * tiles_for_rank(width, height, 0, world)) * 4096 * 4
+        g = self._dev(gathered4, "gathered4", _F32, need)
+        arr = (C.c_void_p * planes)(*[self._dev(f, "frames4", _F32, width * height * 4) for f in frames4])
+        fn = self.lib.vct_untile_planes_packed_device if packed else self.lib.vct_untile_planes_device
+        self._check(fn(self.h, g, planes, width, height, world, C.cast(arr, C.c_void_p)), "untile_planes_device")
+
+    # -- one process per GPU over RCCL (vct_comm_*, SURVEY.md 8e) -----------
+    @staticmethod
+    def comm_get_id(lib=None) -> bytes:
+        lib = lib if lib is not None else _lib.load()
+        cid = VctCommId()
+        st = lib.vct_comm_get_id(C.byref(cid))
+        if st != 0:
+            raise VctError(st, "vct_comm_get_id")
+        return C.string_at(C.addressof(cid), 128)
+
+    def comm_init(self, comm_id: bytes, nranks: int, rank: int):
+        cid = VctCommId()
+        C.memmove(C.addressof(cid), comm_id, 128)
+        self._check(self.lib.vct_comm_init(self.h, C.byref(cid), nranks, rank), "comm_init")
+
+    def comm_broadcast_level0(self, root: int = 0):
+        self._check(self.lib.vct_comm_broadcast_level0(self.h, root), "comm_broadcast_level0")
+
+    def comm_trace_frame(self, pos4, nrm4, alb4, width, height, eye, diffuse4, spec4, root=0,
+                         cone_steps=None, variant=0):
+        """Trace this rank's tiles and assemble the frame on `root` (VCT_ALL_RANKS: every rank)."""
+        a = VctTraceArgs()
+        px = width * height
+        a.pos4 = self._dev(pos4, "pos4", _F32, 4 * px)
+        a.nrm4 = self._dev(nrm4, "nrm4", _F32, 4 * px)
+        a.alb4 = self._dev(alb4, "alb4", _F32, 4 * px)
+        a.width, a.height = width, height
+        a.eye = _f3(eye)
+        a.diffuse4 = self._dev(diffuse4, "diffuse4", _F32, 4 * px)
+        a.spec4 = self._dev(spec4, "spec4", _F32, 4 * px)
+        a.cone_steps = self._dev(cone_steps, "cone_steps", _I64, 1)
+        a.variant = variant
+        self._check(self.lib.vct_comm_trace_frame(self.h, C.byref(a), root), "comm_trace_frame")
+
+    def comm_destroy(self):
+        self._check(self.lib.vct_comm_destroy(self.h), "comm_destroy")
+
+    def _gbuf_ptrs(self, width, height, pos4, nrm4, alb4):
+        n = 4 * width * height
+        return self._dev(pos4, "pos4", _F32, n), self._dev(nrm4, "nrm4", _F32, n), self._dev(alb4, "alb4", _F32, n)
 
     def gbuffer_raycast_device(self, cam, width, height, roughness, pos4, nrm4, alb4):
         c = cam.to_ctypes() if hasattr(cam, "to_ctypes") else cam
-        ptr = lambda t: t if isinstance(t, int) else t.data_ptr()
         self._check(self.lib.vct_gbuffer_raycast_device(self.h, C.byref(c), width, height, float(roughness),
-                                                        ptr(pos4), ptr(nrm4), ptr(alb4)), "raycast")
+                                                        *self._gbuf_ptrs(width, height, pos4, nrm4, alb4)),
+                    "raycast")
 
     def gbuffer_raster_device(self, cam, width, height, roughness, pos4, nrm4, alb4):
         """Row f2: tile-binned G-buffer pass (same output as gbuffer_raycast_device)."""
         c = cam.to_ctypes() if hasattr(cam, "to_ctypes") else cam
-        ptr = lambda t: t if isinstance(t, int) else t.data_ptr()
         self._check(self.lib.vct_gbuffer_raster_device(self.h, C.byref(c), width, height, float(roughness),
-                                                       ptr(pos4), ptr(nrm4), ptr(alb4)), "raster")
+                                                       *self._gbuf_ptrs(width, height, pos4, nrm4, alb4)),
+                    "raster")
 
     def composite_device(self, pos4, nrm4, alb4, diffuse4, spec4, width, height, dir_to_light,
                          color=(1.0, 1.0, 1.0), out_linear4=None, out_rgba8=None):
         """Row f3 composite + present on device buffers (torch tensors or raw pointers)."""
-        ptr = lambda t: None if t is None else (t if isinstance(t, int) else t.data_ptr())
         l = (C.c_float * 3)(*[float(x) for x in dir_to_light])
         c = (C.c_float * 3)(*[float(x) for x in color])
-        self._check(self.lib.vct_composite_device(self.h, ptr(pos4), ptr(nrm4), ptr(alb4), ptr(diffuse4),
-                                                  ptr(spec4), width, height, l, c, ptr(out_linear4),
-                                                  ptr(out_rgba8)), "composite")
+        n = 4 * width * height
+        self._check(self.lib.vct_composite_device(
+            self.h, *self._gbuf_ptrs(width, height, pos4, nrm4, alb4), self._dev(diffuse4, "diffuse4", _F32, n),
+            self._dev(spec4, "spec4", _F32, n), width, height, l, c, self._dev(out_linear4, "out_linear4", _F32, n),
+            self._dev(out_rgba8, "out_rgba8", _I32, width * height)), "composite")
 
     # -- grid access ------------------------------------------------------
     def download_level(self, level: int, face: int = 0) -> np.ndarray:
@@ -250,11 +356,11 @@ class Context:
         return p.value, b.value
 
     def copy_level0_to_device(self, dst):
-        ptr = dst if isinstance(dst, int) else dst.data_ptr()
+        ptr = self._dev(dst, "dst", _F32, 4 * self.n ** 3)
         self._check(self.lib.vct_copy_level0_to_device(self.h, ptr), "copy_level0_to_device")
 
     def set_level0_from_device(self, src):
-        ptr = src if isinstance(src, int) else src.data_ptr()
+        ptr = self._dev(src, "src", _F32, 4 * self.n ** 3)
         self._check(self.lib.vct_set_level0_from_device(self.h, ptr), "set_level0_from_device")
 
     def download_voxels(self):

@@ -17,7 +17,9 @@ EXPORTS = (
     "vct_create", "vct_destroy", "vct_last_error", "vct_status_string", "vct_abi_version",
     "vct_get_config", "vct_set_stream", "vct_synchronize", "vct_create_multi", "vct_num_devices", "vct_voxelize", "vct_voxelize_device",
     "vct_inject_directional", "vct_build_mips", "vct_trace", "vct_trace_device",
-    "vct_tiles_for_rank", "vct_untile_device", "vct_untile_planes_device", "vct_gbuffer_raycast_device", "vct_gbuffer_raster_device",
+    "vct_tiles_for_rank", "vct_untile_device", "vct_untile_planes_device", "vct_untile_planes_packed_device",
+    "vct_tile_offset", "vct_comm_get_id", "vct_comm_init", "vct_comm_rank", "vct_comm_broadcast_level0",
+    "vct_comm_trace_frame", "vct_comm_destroy", "vct_gbuffer_raycast_device", "vct_gbuffer_raster_device",
     "vct_composite_device",
     "vct_num_levels", "vct_level_dims", "vct_download_level", "vct_upload_level0",
     "vct_level0_device", "vct_copy_level0_to_device", "vct_set_level0_from_device",
@@ -49,6 +51,13 @@ class VctCamera(C.Structure):
         ("near_plane", C.c_float),
         ("far_plane", C.c_float),
     ]
+
+
+class VctCommId(C.Structure):
+    _fields_ = [("internal", C.c_char * 128)]
+
+
+VCT_ALL_RANKS = -1
 
 
 class VctTraceArgs(C.Structure):
@@ -113,6 +122,14 @@ def bind(lib: C.CDLL) -> C.CDLL:
         "vct_tiles_for_rank": (u32, [u32, u32, u32, u32]),
         "vct_untile_device": (i32, [P, P, u32, u32, u32, P]),
         "vct_untile_planes_device": (i32, [P, P, u32, u32, u32, u32, P]),
+        "vct_untile_planes_packed_device": (i32, [P, P, u32, u32, u32, u32, P]),
+        "vct_tile_offset": (u32, [u32, u32, u32, u32]),
+        "vct_comm_get_id": (i32, [P]),
+        "vct_comm_init": (i32, [P, P, u32, u32]),
+        "vct_comm_rank": (i32, [P, C.POINTER(u32), C.POINTER(u32)]),
+        "vct_comm_broadcast_level0": (i32, [P, u32]),
+        "vct_comm_trace_frame": (i32, [P, C.POINTER(VctTraceArgs), i32]),
+        "vct_comm_destroy": (i32, [P]),
         "vct_gbuffer_raycast_device": (i32, [P, C.POINTER(VctCamera), u32, u32, f32, P, P, P]),
         "vct_gbuffer_raster_device": (i32, [P, C.POINTER(VctCamera), u32, u32, f32, P, P, P]),
         "vct_composite_device": (i32, [P, P, P, P, P, P, u32, u32, C.POINTER(f32), C.POINTER(f32), P, P]),

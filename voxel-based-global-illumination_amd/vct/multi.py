@@ -2,15 +2,25 @@
 
 The framebuffer is cut into 64x64 tiles; tile t belongs to rank t % world
 (interleaved, so background and early-out variance spread evenly).  Each rank
-writes its tiles to a rank-compact buffer [max_tiles][64*64][4] (max_tiles =
-tiles of rank 0, the largest share, so every rank's buffer has the same size
-for all_gather); the all-gathered [world][max_tiles][64*64][4] buffer is
-scattered back into the frame (vct_untile_device on the GPU, :func:`untile`
-here on the host).
+writes its tiles to a rank-compact buffer, and the frame is assembled from the
+ranks' buffers in one of two ways:
+
+* ``present`` (default): every rank sends exactly its own tiles to the
+  presenting rank (RCCL send / recv; each rank's bytes cross its own xGMI
+  link once), which un-permutes the packed buffer (rank r's
+  [planes][tiles(r)*64*64] block at tile offset planes * tile_offset(r)).
+  Only the presenting rank holds the frame, as a renderer presents from one
+  GPU.
+* ``allgather`` (the north_star collective): rank buffers padded to rank 0's
+  share ([max_tiles][64*64][4]) are all-gathered, and every rank un-permutes
+  the whole [world][planes][max_tiles*64*64] buffer.
+
+vct_untile_planes(_packed)_device does the un-permute on the GPU;
+:func:`untile` / :func:`untile_packed` are the host mirrors.
 
 :class:`FrameTracer` is the per-rank driver bench.py uses: one process per GPU,
 torch.distributed over RCCL ("nccl") for the level-0 grid broadcast and the
-framebuffer all-gather.
+frame exchange.
 """
 from __future__ import annotations
 
@@ -57,6 +67,27 @@ def pack(frame: np.ndarray, rank: int, world: int) -> np.ndarray:
     return out
 
 
+def tile_offset(w: int, h: int, rank: int, world: int) -> int:
+    """Tiles of ranks 0..rank-1: rank * q + min(rank, T mod world) (vct_tile_offset)."""
+    world = max(world, 1)
+    _, _, total = num_tiles(w, h)
+    q, rem = divmod(total, world)
+    return 0 if rank >= world else rank * q + min(rank, rem)
+
+
+def untile_packed(packed: np.ndarray, w: int, h: int, world: int, planes: int) -> list:
+    """Packed [sum_r planes*tiles(r)*64*64][C] -> planes x [h][w][C] (host mirror of
+    vct_untile_planes_packed_device)."""
+    C = packed.shape[1:]
+    outs = [np.zeros((h * w,) + C, packed.dtype) for _ in range(planes)]
+    for r in range(world):
+        fi, ci = compact_index(w, h, r, world)
+        base, nt = planes * tile_offset(w, h, r, world), tiles_for_rank(w, h, r, world)
+        for p in range(planes):
+            outs[p][fi] = packed[(base + p * nt) * TILE * TILE + ci]
+    return [o.reshape((h, w) + C) for o in outs]
+
+
 def untile(gathered: np.ndarray, w: int, h: int, world: int) -> np.ndarray:
     """[world][max_tiles*64*64][C] -> [h][w][C] (host mirror of vct_untile_device)."""
     C = gathered.shape[2:]
@@ -68,35 +99,60 @@ def untile(gathered: np.ndarray, w: int, h: int, world: int) -> np.ndarray:
 
 
 class FrameTracer:
-    """Per-rank K4 driver: trace own tiles, all-gather, un-permute (torch + RCCL).
+    """Per-rank K4 driver: trace own tiles, exchange, un-permute (torch + RCCL).
 
-    Each rank traces its tiles into one rank-compact buffer holding the diffuse
-    and the specular plane side by side ([2][max_tiles*64*64][4]), so ONE
-    all-gather moves both; one vct_untile_planes_device launch scatters them.
+    mode "present": rank r traces its tiles into [2][tiles(r)*64*64][4]
+    (diffuse plane, then specular plane) and sends exactly that to the
+    presenting rank `root`, which traces its own tiles straight into its slice
+    of the packed receive buffer; one packed two-plane untile assembles the
+    frame on `root` only.  mode "allgather": buffers padded to rank 0's share,
+    ONE all-gather moves both planes to every rank, one two-plane untile each.
     With one rank there is nothing to exchange: the trace writes the frame.
 
     :meth:`frame` is one synchronous frame.  :meth:`step` / :meth:`drain` run
-    frames as a pipeline (RCCL only): the all-gather of frame f runs on the
+    frames as a pipeline (RCCL only): the exchange of frame f runs on the
     process group's stream while frame f+1 is traced, and frame f is
     un-permuted after that trace was queued.  Two buffer sets alternate; the
-    stream order (trace f+1, wait gather f, untile f, trace f+2, ...) keeps a
-    buffer from being overwritten before its gather and untile have read it.
+    stream order (trace f+1, wait exchange f, untile f, trace f+2, ...) keeps a
+    buffer from being overwritten before its exchange and untile have read it.
     """
 
-    def __init__(self, ctx, torch, dist, w: int, h: int, rank: int, world: int, device):
+    def __init__(self, ctx, torch, dist, w: int, h: int, rank: int, world: int, device, mode: str = "present",
+                 root: int = 0):
+        if mode not in ("present", "allgather"):
+            raise ValueError(f"mode {mode!r}: 'present' or 'allgather'")
         self.ctx, self.torch, self.dist = ctx, torch, dist
         self.w, self.h, self.rank, self.world = w, h, rank, world
+        self.mode, self.root = mode, root
         self.max_tiles = tiles_for_rank(w, h, 0, world)
-        self.npx = self.max_tiles * TILE * TILE
+        self.my_tiles = tiles_for_rank(w, h, rank, world)
+        _, _, self.total_tiles = num_tiles(w, h)
         f32 = torch.float32
         nsets = 2 if world > 1 else 1
-        self.comp = [torch.zeros((2, self.npx, 4), dtype=f32, device=device) for _ in range(nsets)]
-        self.gath = [torch.empty((world, 2, self.npx, 4), dtype=f32, device=device) for _ in range(nsets)] \
-            if world > 1 else []
+        tpx = TILE * TILE
+        self.comp, self.gath = [], []
+        if world > 1 and mode == "allgather":
+            self.npx = self.max_tiles * tpx
+            self.comp = [torch.zeros((2, self.npx, 4), dtype=f32, device=device) for _ in range(nsets)]
+            self.gath = [torch.empty((world, 2, self.npx, 4), dtype=f32, device=device) for _ in range(nsets)]
+        elif world > 1:
+            self.npx = self.my_tiles * tpx
+            if rank == root:     # packed receive buffer; the root's own slice is its trace target
+                self.gath = [torch.zeros((2 * self.total_tiles * tpx, 4), dtype=f32, device=device)
+                             for _ in range(nsets)]
+                off = 2 * tile_offset(w, h, rank, world) * tpx
+                self.comp = [g[off:off + 2 * self.npx].view(2, self.npx, 4) for g in self.gath]
+            else:
+                self.comp = [torch.zeros((2, self.npx, 4), dtype=f32, device=device) for _ in range(nsets)]
         self.diff = torch.zeros((h, w, 4), dtype=f32, device=device)
         self.spec = torch.zeros((h, w, 4), dtype=f32, device=device)
         self.cur = 0
         self.pending = None
+
+    @property
+    def holds_frame(self) -> bool:
+        """True where the assembled frame lands (every rank for allgather)."""
+        return self.world == 1 or self.mode == "allgather" or self.rank == self.root
 
     def trace_local(self, gb, eye, cone_steps=None, texel_fetches=None, steps_px=None, variant=0, buf=0):
         pos, nrm, alb = gb
@@ -105,27 +161,59 @@ class FrameTracer:
                                   steps_px=steps_px, cone_steps=cone_steps, texel_fetches=texel_fetches,
                                   variant=variant)
             return
+        if self.my_tiles == 0:
+            return
         c = self.comp[buf]
         self.ctx.trace_device(pos, nrm, alb, self.w, self.h, eye, c[0], c[1],
                               steps_px=steps_px, cone_steps=cone_steps, texel_fetches=texel_fetches,
                               tile_rank=self.rank, tile_world=self.world, tile_compact=True, variant=variant)
 
-    def _pipelined(self):
-        return self.world > 1 and self.dist.get_backend() == "nccl"
+    def _nccl(self):
+        return self.dist.get_backend() == "nccl"
 
-    def _gather(self, buf, async_op):
-        if self.dist.get_backend() == "nccl":            # RCCL over xGMI
-            return self.dist.all_gather_into_tensor(self.gath[buf], self.comp[buf], async_op=async_op)
-        # gloo (CPU-side rehearsal of the same path)
-        self.dist.all_gather(list(self.gath[buf].unbind(0)), self.comp[buf])
-        return None
+    def _pipelined(self):
+        return self.world > 1 and self._nccl()
+
+    def _exchange(self, buf, async_op):
+        """Moves frame `buf`'s tiles; returns the outstanding works (async RCCL) or []."""
+        d = self.dist
+        if self.mode == "allgather":
+            if self._nccl():                                 # RCCL over xGMI
+                w = d.all_gather_into_tensor(self.gath[buf], self.comp[buf], async_op=async_op)
+                return [w] if async_op else []
+            d.all_gather(list(self.gath[buf].unbind(0)), self.comp[buf])   # gloo (CPU rehearsal)
+            return []
+        tpx = TILE * TILE
+        ops = []
+        if self.rank == self.root:
+            for r in range(self.world):
+                nt = tiles_for_rank(self.w, self.h, r, self.world)
+                if r == self.root or nt == 0:
+                    continue
+                off = 2 * tile_offset(self.w, self.h, r, self.world) * tpx
+                ops.append(d.P2POp(d.irecv, self.gath[buf][off:off + 2 * nt * tpx], r))
+        elif self.my_tiles:
+            ops.append(d.P2POp(d.isend, self.comp[buf].view(-1, 4), self.root))
+        if not ops:
+            return []
+        works = d.batch_isend_irecv(ops)
+        if not async_op:
+            for w in works:
+                w.wait()
+            return []
+        return works
 
     def _untile(self, buf):
-        self.ctx.untile_planes_device(self.gath[buf], self.w, self.h, self.world, (self.diff, self.spec))
+        if self.mode == "allgather":
+            self.ctx.untile_planes_device(self.gath[buf], self.w, self.h, self.world, (self.diff, self.spec))
+        elif self.rank == self.root:
+            self.ctx.untile_planes_device(self.gath[buf], self.w, self.h, self.world, (self.diff, self.spec),
+                                          packed=True)
 
     def gather(self, buf=0):
+        """The exchange and the untile of buffer set `buf`, synchronously (also timed alone)."""
         if self.world > 1:
-            self._gather(buf, False)
+            self._exchange(buf, False)
             self._untile(buf)
 
     def frame(self, gb, eye, variant=0):
@@ -147,13 +235,44 @@ class FrameTracer:
         self.trace_local(gb, eye, variant=variant, buf=b)
         if on_traced:
             on_traced()
-        work = self._gather(b, True)
+        works = self._exchange(b, True)
         self.drain()
-        self.pending = (work, b)
+        self.pending = (works, b)
 
     def drain(self):
         if self.pending is not None:
-            work, b = self.pending
+            works, b = self.pending
             self.pending = None
-            work.wait()                                     # current stream waits for the gather
+            for w in works:
+                w.wait()                                    # current stream waits for the exchange
             self._untile(b)
+
+
+class PatternContext:
+    """Stand-in for a vct Context in multi-rank rehearsals without a GPU
+    (bench.py --dry-run, tests): its "trace" writes each owned pixel's frame index
+    (diffuse plane) and its negative (specular plane) into the rank's compact
+    tiles, and its untile is the host mirror above, so an assembled frame can be
+    checked exactly.  Nothing is measured with it."""
+
+    def __init__(self, torch):
+        self.torch = torch
+
+    def trace_device(self, pos4, nrm4, alb4, width, height, eye, diffuse4, spec4, tile_rank=0, tile_world=1,
+                     tile_compact=False, **_):
+        t = self.torch
+        fi, ci = compact_index(width, height, tile_rank, tile_world) if tile_compact else \
+            (np.arange(width * height), np.arange(width * height))
+        v = t.from_numpy(fi.astype(np.float32))[:, None].expand(-1, 4)
+        diffuse4.view(-1, 4)[t.from_numpy(ci)] = v
+        spec4.view(-1, 4)[t.from_numpy(ci)] = -v
+
+    def untile_planes_device(self, gathered4, width, height, world, frames4, packed=False):
+        g = gathered4.reshape(-1, 4).numpy()
+        if packed:
+            outs = untile_packed(g, width, height, world, len(frames4))
+        else:
+            gg = g.reshape(world, len(frames4), -1, 4)
+            outs = [untile(gg[:, p], width, height, world) for p in range(len(frames4))]
+        for f, o in zip(frames4, outs):
+            f.copy_(self.torch.from_numpy(o))
