@@ -165,7 +165,7 @@ def load_profile(path, key):
 def roofline(rec, reason, k4_ms, texels, valid_px, profile_path, key):
     gather = texels * BYTES_PER_TEXEL + valid_px * BYTES_PER_VALID_PX
     t = k4_ms * 1e-3
-    out = {"bound": "issue", "achieved": None, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s", "frac": None,
+    out = {"bound": "issue (VALU)", "achieved": None, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s", "frac": None,
            "traffic": None, "gather_bytes": gather, "gather_GBs": round(gather / t / 1e9, 1),
            "texel_fetches_per_launch": texels,
            "peak_basis": "1024 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
@@ -187,9 +187,15 @@ def roofline(rec, reason, k4_ms, texels, valid_px, profile_path, key):
         "profile": f"{os.path.relpath(profile_path, REPO)}#{key}",
         "profile_kernel_ms": rec.get("duration_ms"),
     })
-    if out["hbm"]["frac"] > out["frac"]:          # name the resource that binds
+    out["valu"] = {"achieved": out["achieved"], "peak": VALU_PEAK_G, "unit": out["unit"], "frac": out["frac"]}
+    # name the resource that binds: the most loaded of VALU issue, scalar issue and HBM
+    if out["salu"]["frac"] > max(out["frac"], out["hbm"]["frac"]):
+        out.update({"bound": "issue (scalar)", "achieved": out["salu"]["achieved"], "peak": SALU_PEAK_G,
+                    "unit": "G SALU instr/s", "frac": out["salu"]["frac"],
+                    "peak_basis": "256 CUs x 2.4 GHz x one scalar instruction per cycle per CU"})
+    elif out["hbm"]["frac"] > out["frac"]:
         out.update({"bound": "hbm", "achieved": round(h_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": out["hbm"]["frac"], "valu_frac": round(v_ach / VALU_PEAK_G, 4)})
+                    "frac": out["hbm"]["frac"], "peak_basis": "HBM3E 8 TB/s spec"})
     return out
 
 

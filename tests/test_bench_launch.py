@@ -55,9 +55,13 @@ def test_roofline_from_profile(tmp_path):
     got, why = bench.load_profile(str(p), key)
     assert got == rec and why is None
     r = bench.roofline(got, why, 1.0, 1000, 10, str(p), key)
-    assert r["bound"] == "issue" and r["frac"] == pytest.approx(6.0e8 / 1e-3 / 1e9 / bench.VALU_PEAK_G, abs=1e-4)
+    assert r["bound"] == "issue (VALU)" and r["frac"] == pytest.approx(6.0e8 / 1e-3 / 1e9 / bench.VALU_PEAK_G, abs=1e-4)
     assert 0 < r["frac"] <= 1 and r["hbm"]["frac"] == pytest.approx(0.7 / 8.0, abs=1e-4)
     assert r["gather_bytes"] == 1000 * 16 + 10 * 80
+    r = bench.roofline(dict(rec, SQ_INSTS_SALU=5.0e8), None, 1.0, 1000, 10, str(p), key)
+    assert r["bound"] == "issue (scalar)" and r["frac"] == pytest.approx(5.0e8 / 1e-3 / 1e9 / bench.SALU_PEAK_G, abs=1e-4)
+    r = bench.roofline(dict(rec, hbm_bytes_per_launch=7.9e9), None, 1.0, 1000, 10, str(p), key)
+    assert r["bound"] == "hbm" and r["frac"] == pytest.approx(7.9 / 8.0, abs=1e-4)
     p.write_text(json.dumps({key: dict(rec, lib_sha256="0" * 64)}))
     got, why = bench.load_profile(str(p), key)
     assert got is None and "another library build" in why
