@@ -28,6 +28,22 @@ int vcth_mesh(const vcth_model* m, uint32_t i, const void** verts, uint32_t* n_v
 /* Material i: name, Ka/Kd/Ks (r, g, b, 1). */
 int vcth_material(const vcth_model* m, uint32_t i, const char** name, float ka[4], float kd[4], float ks[4]);
 void vcth_free(vcth_model* m);
+/* Apply a column-major 4x4 model matrix to every vertex position (host Model::Transform). */
+void vcth_transform(vcth_model* m, const float mat[16]);
+/* Vertex-position bounds; returns 0, or -1 for an empty model. */
+int vcth_bounds(const vcth_model* m, float lo[3], float hi[3]);
+
+/* The reference's model matrix, r_voxelization.cpp:26-29 (column-major). */
+void vcth_reference_model_matrix(float mat[16]);
+/* Cubic grid around [lo, hi], one voxel of padding per side at resolution n. */
+void vcth_grid_for_bounds(const float lo[3], const float hi[3], uint32_t n, float aabb_min[3], float* extent);
+
+/* The host FPS camera (host/camera.cpp = the reference Camera, scene/camera.cpp)
+ * built from init = (pos x, y, z, yaw, pitch), then n_ops operations: kind[i] in
+ * 'm' ProcessMouseMovement(a, b), 's' ProcessMouseScroll(a), 'f' / 'b' / 'l' / 'r'
+ * ProcessKeyboard(FORWARD / BACKWARD / LEFT / RIGHT, a).  out[15] = Position,
+ * Front, Right, Up, Yaw, Pitch, Zoom. */
+int vcth_camera_eval(const float init[5], const char* kinds, const float* a, const float* b, int n_ops, float out[15]);
 
 #ifdef __cplusplus
 }

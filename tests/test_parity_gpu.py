@@ -684,7 +684,8 @@ def test_cpp_host_renderer_slot(gpu_ready, tmp_path):
     runs = []
     for r in range(2):
         out = str(tmp_path / f"frame{r}.ppm")
-        p = subprocess.run([exe, obj, str(n), str(w), str(h), "3", out], capture_output=True, text=True, timeout=120)
+        p = subprocess.run([exe, obj, str(n), str(w), str(h), "3", out, "--model=identity", "--grid=unit"],
+                           capture_output=True, text=True, timeout=120)
         assert p.returncode == 0, p.stderr
         steps = [int(x) for x in re.findall(r"(\d+) cone steps", p.stdout)]
         assert len(steps) == 3 and len(set(steps)) == 1 and steps[0] > 0, p.stdout
@@ -695,7 +696,8 @@ def test_cpp_host_renderer_slot(gpu_ready, tmp_path):
     assert runs[0][0] == runs[1][0] and np.array_equal(runs[0][1], runs[1][1])
     # the same host driving three device ranks through vct_create_multi: the same image
     out = str(tmp_path / "frame_multi.ppm")
-    p = subprocess.run([exe, obj, str(n), str(w), str(h), "2", out, "3"], capture_output=True, text=True, timeout=120)
+    p = subprocess.run([exe, obj, str(n), str(w), str(h), "2", out, "3", "--model=identity", "--grid=unit"],
+                       capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr
     assert [int(x) for x in re.findall(r"(\d+) cone steps", p.stdout)] == [runs[0][0]] * 2, p.stdout
     assert open(out, "rb").read() == open(str(tmp_path / "frame0.ppm"), "rb").read()
@@ -769,3 +771,97 @@ def test_multi_device_context(gpu_ready, devices):
             ctx.trace_device(*gb, w, h, cam.position, d, d.clone(), tile_rank=0, tile_world=2)
     ctx.close()
     ref.close()
+
+
+def test_cpp_host_reference_placement(gpu_ready, tmp_path):
+    """ConeTraceRenderer with the reference's draw placement (host/main.cpp defaults):
+    the model matrix T(0,-1.75,0) S(0.2) of r_voxelization.cpp:26-29 applied before
+    K1 and the grid fitted around the placed model.  The host's grid equals
+    vcth_grid_for_bounds of the placed bounds, and its frames take the cone steps of
+    the Python path voxelizing the same placed vertices (host loader + host
+    transform) in that grid (within 1 %: float vs double camera vectors)."""
+    import os
+    import re
+    import subprocess
+    import torch
+    import host_lib
+    from helpers import write_obj
+    from vct import Context, scenes
+    from vct.camera import Camera, reference_model_matrix
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "voxel-based-global-illumination_amd", "build", "vct_headless")
+    s = scenes.atrium()
+    s.verts = [[5.0 * r[0], 5.0 * r[1], 5.0 * r[2]] + list(r[3:]) for r in s.verts]   # nanosuit-sized: y in [-2.75, -0.75] after M
+    obj = write_obj(s, str(tmp_path))
+    n, w, h = 64, 160, 120
+    p = subprocess.run([exe, obj, str(n), str(w), str(h), "2", str(tmp_path / "placed.ppm")], capture_output=True,
+                       text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    g = re.search(r"aabb_min (\S+) (\S+) (\S+) extent (\S+)", p.stdout)
+    g0 = [float.fromhex(x) for x in g.groups()[:3]]
+    E = float.fromhex(g.group(4))
+    steps = [int(x) for x in re.findall(r"(\d+) cone steps", p.stdout)]
+    v, i, m, k, lo, hi = host_lib.load_placed(obj, reference_model_matrix())
+    assert lo[1] >= np.float32(-2.75) - 1e-5 and hi[1] <= np.float32(-0.75) + 1e-5
+    hg0, hE = host_lib.grid_for_bounds(lo, hi, n)
+    assert np.array_equal(np.float32(g0), hg0) and np.float32(E) == np.float32(hE)
+    ctx = Context(n, g0, E)
+    ctx.voxelize(v, i, m, k)
+    ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    ctx.build_mips()
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    gb = [torch.empty((h, w, 4), device=dev) for _ in range(3)]
+    cam = Camera()
+    ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)
+    d, sp = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.trace_device(*gb, w, h, cam.position, d, sp, cone_steps=cnt)
+    torch.cuda.synchronize()
+    pos = gb[0].cpu().numpy()
+    hit = pos[..., 3] != 0
+    assert hit.sum() > 0.05 * w * h                  # the placed model is in view
+    assert pos[hit][:, 1].max() <= hi[1] + 1e-4      # every hit lies on the moved geometry
+    assert steps and len(set(steps)) == 1 and abs(int(cnt.item()) - steps[0]) <= 0.01 * steps[0]
+    ctx.close()
+
+
+@pytest.mark.parametrize("case,size", [(0, "200x130"), (1, "160x120"), (2, "64x48"), (5, "200x130")])
+def test_gbuffer_projects_to_pixel_centres(gpu_ready, case, size):
+    """The G-buffer pass against the reference camera: every hit position of the HIP
+    raster pass, projected through GLM's perspective(radians(Zoom), w/h, 0.1, 100) and
+    lookAt view matrix of the reference Camera (tests/golden/ref_camera.json, from the
+    reference's own camera.cpp + GLM), lands on its pixel centre within 1e-3 px
+    (row 0 = top).  The camera is the fixture's Position/Front/Up/Right/Zoom."""
+    import json
+    import os
+    import torch
+    from vct import VctCamera, scenes
+    fix = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_camera.json")))
+    c = fix["cameras"][case]
+    hx = lambda v: np.array([float.fromhex(x) for x in v], np.float64)
+    w, h = (int(x) for x in size.split("x"))
+    ctx, s, arrs, (g0, E) = gpu_pipeline(32, "atrium")
+    vc = VctCamera()
+    vc.position[:], vc.front[:] = list(hx(c["position"])), list(hx(c["front"]))
+    vc.up[:], vc.right[:] = list(hx(c["up"])), list(hx(c["right"]))
+    vc.zoom_deg, vc.near_plane, vc.far_plane = float.fromhex(c["zoom"]), 0.1, 100.0
+    dev = torch.device("cuda")
+    gb = [torch.zeros((h, w, 4), device=dev) for _ in range(3)]
+    ctx.gbuffer_raster_device(vc, w, h, scenes.ROUGHNESS, *gb)
+    torch.cuda.synchronize()
+    pos = gb[0].cpu().numpy().astype(np.float64)
+    hit = pos[..., 3] != 0
+    assert hit.sum() > 0.2 * w * h
+    V = hx(c["view"]).reshape(4, 4).T
+    P = hx(c["proj"][size]).reshape(4, 4).T
+    ys, xs = np.nonzero(hit)
+    p4 = np.concatenate([pos[ys, xs, :3], np.ones((len(xs), 1))], 1)
+    clip = p4 @ (P @ V).T
+    ndc = clip[:, :3] / clip[:, 3:4]
+    px = (ndc[:, 0] + 1.0) * 0.5 * w
+    py = (1.0 - ndc[:, 1]) * 0.5 * h
+    err = np.maximum(np.abs(px - (xs + 0.5)), np.abs(py - (ys + 0.5)))
+    assert err.max() <= 1e-3, (err.max(), np.argmax(err))
+    assert np.all((ndc[:, 2] > -1) & (ndc[:, 2] < 1))     # inside GLM's depth range (near 0.1, far 100)
+    ctx.close()

@@ -34,7 +34,7 @@ def main():
     lib = _lib.load()
     lib.vct_debug_counters.restype = C.c_int
     lib.vct_debug_counters.argtypes = [C.c_void_p, C.c_int]
-    ctr = (C.c_ulonglong * 40)()
+    ctr = (C.c_ulonglong * 48)()
     g0, E = scenes.grid_for_unit_box(a.n)
     ctx = Context(a.n, g0, E)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -63,6 +63,10 @@ def main():
         print(f"variant {v}: level-A brick {c[0]} / gather {c[1]} / staged {c[2]} / cache hit {c[3]}; "
               f"gathers per level: {c[4:15]}")
         print(f"  level-A brick samples: zero brick {c[17]} / nonzero {c[15]}")
+        if not a.clk:
+            print(f"  level B: hit {c[26]} / staged {c[27]} / gather {c[28]} / not sampled {c[31]}; "
+                  f"faces-mode brick samples A {c[29]} / B {c[30]}")
+            print(f"  quadrant bricks: A staged {c[40]} / hit {c[41]}; B staged {c[42]} / hit {c[43]}")
         print(f"  gather reasons: faces not uniform {c[16]}; footprint span (level 0) <=3/<=5/<=9/more {c[18:22]}"
               f"; (level>0) {c[22:26]}")
         if a.clk:

@@ -39,7 +39,7 @@
 // Debug-build counters (make dbg -> vct/libvct_hip_dbg.so, tools/dbg_counters.py):
 // per wave and level sample, which path served it.  Compiled out of the product.
 #if defined(VCT_DEBUG_COUNTERS) || defined(VCT_DEBUG_CLOCK)
-__device__ unsigned long long vct_dbg_ctr[32];
+__device__ unsigned long long vct_dbg_ctr[40];
 __device__ unsigned long long vct_dbg_time[8];
 #endif
 #if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
@@ -130,6 +130,7 @@ struct TraceK {
     unsigned* spec_state;        // [kSpecSlots] 0 building, 1 ready, 2 needs more than 64 rows
     StepRow* spec_rows;          // [kSpecSlots][64]
     int spec_tabs;               // 0: specular cones always derive their steps per lane (variant bit 0x100)
+    int abl0;                    // always 0 (an SGPR the compiler cannot fold: ablation builds only)
     int split;                   // 0: one workgroup per 16x16 block traces every cone; 1: two (diffuse | specular);
                                  // 2: ndp diffuse parts (cones [g * nd_chunk, ...)) | specular
     int nd_chunk;                // split 2: diffuse cones per part (part g: [g * nd_chunk, (g + 1) * nd_chunk) & nd)
@@ -174,7 +175,10 @@ __device__ __forceinline__ float4 combine3(float wx, float wy, float wz, float4 
 }
 
 // corners whose three anisotropic faces are in registers at once (VGPR budget)
-constexpr int kCh = 4;
+#ifndef VCT_KCH
+#define VCT_KCH 4
+#endif
+constexpr int kCh = VCT_KCH;
 
 // trilinear corner weights (x fastest), w_c = (wx * wy) * wz
 __device__ __forceinline__ void corner_weights(float fx, float fy, float fz, float (&wc)[8]) {
@@ -199,11 +203,17 @@ struct LevelView<true> {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, in ? i << 4 : 0xfffffff0u, 0, 0);
         return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
     }
+    // ablation: the same load again (soffset = an opaque 0), its value kept alive unused
+    __device__ void twin(uint32_t i, bool in, int z) const {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, in ? i << 4 : 0xfffffff0u, z, 0);
+        asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+    }
 };
 
 template <>
 struct LevelView<false> {
     const float4* p;
+    __device__ void twin(uint32_t, bool, int) const {}
     __device__ float4 fetch(uint32_t i, bool in) const {
         const float4 v = p[in ? i : 0u];
         return sel4(in, v, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
@@ -267,6 +277,19 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
         else return level_view_lane(k, l);
     }();
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#ifdef VCT_ABL_GATHER
+    if constexpr (UNIF) {
+        const uint32_t vl0 = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            lv.twin(idx[c], in[c], k.abl0);
+            if (l > 0 && k.aniso) {
+                lv.twin((uint32_t)fy * vl0 + idx[c], in[c], k.abl0);
+                lv.twin((uint32_t)fz * vl0 + idx[c], in[c], k.abl0);
+            }
+        }
+    }
+#endif
     if (l == 0 || !k.aniso) {
         float4 v[8];
 #pragma unroll
@@ -370,7 +393,12 @@ template <bool UNION> constexpr int entry_slots() { return (UNION ? 4 : 3) * kBl
 // writes): the asm "memory" clobber keeps the compiler from moving DS ops
 // across it, lgkmcnt(0) makes it explicit in hardware.
 __device__ __forceinline__ void wave_lds_sync() {
+#ifdef VCT_LDS_NOWAIT
+    // LDS instructions of one wave execute in order: a compiler fence suffices
+    asm volatile("" ::: "memory");
+#else
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -387,15 +415,17 @@ struct BrickEntry {
     int lvl;                     // staged level (-1 = empty)
     int ox, oy, oz;              // its origin
     int zero;                    // every staged texel is +0: any sample from it is exactly (+0, +0, +0, +0)
+    int quad;                    // four quadrant bricks (origins per lane: BrickCache::qa / qb)
 };
 // The cache holds the bricks of the step's two levels: `a` for level l0, `b`
 // for l0 + 1.  A cone's mip level never decreases, so when l0 advances by one
 // the old `b` becomes the new `a` (the two swap, with their LDS regions) and
 // `b` restages; no per-step indexing (a runtime-indexed pair would cost
 // scalar selects on every access).
-struct BrickCache {              // wave-uniform
+struct BrickCache {              // wave-uniform, except the quadrant origins
     BrickEntry a, b;
     int flip;                    // 0: a in LDS region 0, b in region 1; 1: swapped
+    uint32_t qa, qb;             // per lane: packed origin of the lane's quadrant brick in a / b (quad entries)
 };
 
 struct Corner {                  // one lane's trilinear footprint at one level
@@ -441,6 +471,53 @@ __device__ __forceinline__ bool brick_origin(const Corner& c, unsigned long long
     return wall_in(am, in_brick(c, b));
 }
 
+#ifndef VCT_QUAD
+#define VCT_QUAD 0     // measured: A gathers -51 %, K4 +2.3 %
+#endif
+
+// ---------------------------------------------------------------------------
+// Quadrant bricks (iso / comb modes, O32 grids).  With the Morton lane order a
+// 16-lane row of the wave is a 4x4-pixel quadrant.  When the wave's footprint
+// spans more than one 4^3 brick, each quadrant gets its own 4^3 brick in its own
+// block of the entry (the entry holds four blocks for faces mode anyway), and the
+// wave samples all four at once: lane -> block (lane >> 4).  A quadrant's origin
+// is its rows' per-axis minimum (or maximum - 2 toward -axis, the slack ahead of
+// the march), a 16-lane DPP reduction; each lane keeps its quadrant's origin
+// packed in one VGPR (10 bits per axis, bias 4: n <= 512).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int row_min_i32(int v) {   // min over the lane's 16-lane row
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));   // row_half_mirror
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));   // row_mirror
+    return v;
+}
+
+constexpr int kQBias = 4;
+__device__ __forceinline__ int qo_x(uint32_t q) { return (int)(q & 1023u) - kQBias; }
+__device__ __forceinline__ int qo_y(uint32_t q) { return (int)((q >> 10) & 1023u) - kQBias; }
+__device__ __forceinline__ int qo_z(uint32_t q) { return (int)(q >> 20) - kQBias; }
+
+// quadrant origin on one axis (neg: toward -axis); inactive lanes do not count
+__device__ __forceinline__ int quad_axis(int c, bool active, bool neg) {
+    const int v = active ? (neg ? -c : c) : INT_MAX;
+    const int m = row_min_i32(v);
+    return neg ? -m - 2 : m;
+}
+
+// every active lane's footprint inside its quadrant's brick -> packed origin in qo
+__device__ __forceinline__ bool quad_origin(int cx, int cy, int cz, bool active, unsigned long long am, int neg,
+                                            uint32_t& qo) {
+    const int ox = quad_axis(cx, active, neg & 1), oy = quad_axis(cy, active, neg & 2), oz = quad_axis(cz, active, neg & 4);
+    const bool in = max(max((uint32_t)(cx - ox), (uint32_t)(cy - oy)), (uint32_t)(cz - oz)) <= 2u;
+    qo = (uint32_t)(ox + kQBias) | ((uint32_t)(oy + kQBias) << 10) | ((uint32_t)(oz + kQBias) << 20);
+    return (__builtin_amdgcn_ballot_w64(!in) & am) == 0ull;
+}
+
+__device__ __forceinline__ bool in_quad(int cx, int cy, int cz, uint32_t qo) {
+    return max(max((uint32_t)(cx - qo_x(qo)), (uint32_t)(cy - qo_y(qo))), (uint32_t)(cz - qo_z(qo))) <= 2u;
+}
+
 enum { kIso = 0, kComb = 1, kFaces = 2 };
 
 struct Tex4 { float4 a, b, c, d; };
@@ -458,6 +535,14 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
     const LevelView<O32> lv = level_view<O32>(k, l);
     Tex4 t;
     t.b = t.c = t.d = z4;
+#ifdef VCT_ABL_STAGE
+    lv.twin(gi, inb, k.abl0);
+    if (mode != kIso) {
+        const uint32_t vl0 = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
+        lv.twin((uint32_t)cc.f1 * vl0 + gi, inb, k.abl0);
+        lv.twin((uint32_t)cc.f2 * vl0 + gi, inb, k.abl0);
+    }
+#endif
     if (mode == kIso) {
         t.a = lv.fetch(gi, inb);
     } else {
@@ -499,15 +584,63 @@ __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const T
     return nz == 0u;
 }
 
-// D_l from a staged brick: corner 0 at `b`; faces mode reads the lane's own
+// the four quadrant bricks of a quad entry (iso / comb): lane j stages texel
+// (j & 3, (j >> 2) & 3, j >> 4) of every quadrant's brick, quadrant q in block q;
+// returns true when every staged value is +0 (the wave's vote)
+template <bool O32>
+__device__ __forceinline__ bool stage_quad(const TraceK& k, int l, int mode, const ConeCtl& cc, uint32_t qo,
+                                           float4* __restrict__ lds) {
+    const int nl = k.n >> l;
+    const int lane = threadIdx.x & 63;
+    const int tx = lane & 3, ty = (lane >> 2) & 3, tz = lane >> 4;
+    const LevelView<O32> lv = level_view<O32>(k, l);
+    const uint32_t vl = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
+    float4* p = lds + ((lane & 15) + kBz * (lane >> 4));
+    uint32_t nz = 0;
+#pragma unroll
+    for (int h = 0; h < 4; h += 2) {
+        float4 v[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)qo, 16 * (h + i));
+            const int sx = qo_x(q) + tx, sy = qo_y(q) + ty, sz = qo_z(q) + tz;
+            const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
+            const uint32_t gi = (uint32_t)sx + __umul24((uint32_t)nl, (uint32_t)sy + __umul24((uint32_t)nl, (uint32_t)sz));
+            if (mode == kIso) {
+                v[i] = lv.fetch(gi, inb);
+            } else {
+                v[i] = combine3(cc.uwx, cc.uwy, cc.uwz, lv.fetch((uint32_t)cc.f0 * vl + gi, inb),
+                                lv.fetch((uint32_t)cc.f1 * vl + gi, inb), lv.fetch((uint32_t)cc.f2 * vl + gi, inb));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            p[kBlk * (h + i)] = v[i];
+            nz |= bits4(v[i]);
+        }
+    }
+    return wall(nz == 0u);
+}
+
+// slot of the lane's corner 0 in a staged entry: the wave's brick, or the lane's
+// quadrant brick (block lane >> 4) of a quad entry
+__device__ __forceinline__ int brick_slot(const Corner& c, const BrickEntry& be, uint32_t qo) {
+    if (VCT_QUAD && be.quad) {
+        const int lane = threadIdx.x & 63;
+        return __mul24(kBlk, lane >> 4) + (c.ix - qo_x(qo)) + 4 * (c.iy - qo_y(qo)) + __mul24(kBz, c.iz - qo_z(qo));
+    }
+    return (c.ix - be.ox) + 4 * (c.iy - be.oy) + __mul24(kBz, c.iz - be.oz);
+}
+
+// D_l from a staged brick: corner 0 at slot `off`; faces mode reads the lane's own
 // face blocks at float4 offsets bx, by, bz
 template <int KL>   // corners x 3 faces per LDS burst in faces mode
-__device__ __forceinline__ float4 brick_sample(const Corner& c, const BrickEntry& be, bool one_slot, int bx,
+__device__ __forceinline__ float4 brick_sample(const Corner& c, int off, bool one_slot, int bx,
                                                int by, int bz, float wdx, float wdy, float wdz,
                                                const float4* __restrict__ lds) {
     float wc[8];
     corner_weights(c.fx, c.fy, c.fz, wc);
-    const float4* b = lds + ((c.ix - be.ox) + 4 * (c.iy - be.oy) + __mul24(kBz, c.iz - be.oz));
+    const float4* b = lds + off;
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (one_slot) {
         float4 v[8];
@@ -569,13 +702,21 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         bc.a = bc.b;
         bc.b = t;
         bc.flip ^= 1;
+        if (VCT_QUAD) {
+            const uint32_t q = bc.qa;
+            bc.qa = bc.qb;
+            bc.qb = q;
+        }
     }
     float4* ldsA = lds + bc.flip * entry_slots<UNION>();
     float4* ldsB = lds + (bc.flip ^ 1) * entry_slots<UNION>();
     // level A: cached, restaged, or gathered
     const Corner cA = level_corner(l0, qx, qy, qz);
     BrickEntry bA = bc.a;
-    bool useA = bA.lvl == l0 && wall_in(amA, in_brick(cA, bA));
+    const auto fits = [&](const Corner& c, const BrickEntry& be, uint32_t qo) {
+        return (VCT_QUAD && be.quad) ? in_quad(c.ix, c.iy, c.iz, qo) : in_brick(c, be);
+    };
+    bool useA = bA.lvl == l0 && wall_in(amA, fits(cA, bA, bc.qa));
     bool stA = false;
     if (!useA && (modeA != kFaces || faces_ok)) {
         BrickEntry nb{};
@@ -584,6 +725,15 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
             bA = nb;
             bc.a = nb;
             useA = stA = true;
+        } else if (VCT_QUAD && O32 && UNION && modeA != kFaces) {   // one brick per quadrant (four blocks: UNION entries)
+            uint32_t q;
+            if (quad_origin(cA.ix, cA.iy, cA.iz, active, amA, cc.neg, q)) {
+                nb.quad = 1;
+                bA = nb;
+                bc.a = nb;
+                bc.qa = q;
+                useA = stA = true;
+            }
         }
     }
     Corner cB = cA;
@@ -591,7 +741,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     bool useB = false, stB = false;
     if (needB) {
         cB = level_corner(l1, qx, qy, qz);
-        useB = bB.lvl == l1 && wall_in(amB, in_brick(cB, bB));
+        useB = bB.lvl == l1 && wall_in(amB, fits(cB, bB, bc.qb));
         if (!useB && (modeB != kFaces || faces_ok)) {
             BrickEntry nb{};
             nb.lvl = l1;
@@ -599,15 +749,41 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
                 bB = nb;
                 bc.b = nb;
                 useB = stB = true;
+            } else if (VCT_QUAD && O32 && UNION && modeB != kFaces) {
+                uint32_t q;
+                if (quad_origin(cB.ix, cB.iy, cB.iz, activeB, amB, cc.neg, q)) {
+                    nb.quad = 1;
+                    bB = nb;
+                    bc.b = nb;
+                    bc.qb = q;
+                    useB = stB = true;
+                }
             }
         }
     }
+    if (useA && bA.quad) VCT_DBG(stA ? 32 : 33);
+    if (useB && bB.quad) VCT_DBG(stB ? 34 : 35);
     VCT_DBG(useA ? (stA ? 2 : 3) : 1);
+    VCT_DBG(needB ? (useB ? (stB ? 27 : 26) : 28) : 31);   // level B: hit / staged / gathered / not sampled
+    if (useA && modeA == kFaces) VCT_DBG(29);               // brick samples read three faces per corner
+    if (useB && modeB == kFaces) VCT_DBG(30);
     pc.mark(1);
     // a brick whose texels are all +0 (empty space) is marked: its samples are exactly
     // zero (fmaf(w, +0, +0) = +0 through the whole trilinear chain), so hits on it skip
     // the LDS reads and the FMAs
-    if (stA && stB) {
+    if (VCT_QUAD && ((stA && bA.quad) || (stB && bB.quad))) {   // a quad entry: stage the levels one by one
+        if (stA) {
+            const bool z = bA.quad ? stage_quad<O32>(k, l0, modeA, cc, bc.qa, ldsA)
+                                   : wall(stage_store(modeA, cc, stage_load<O32>(k, l0, bA, modeA, cc), ldsA));
+            bA.zero = bc.a.zero = z;
+        }
+        if (stB) {
+            const bool z = bB.quad ? stage_quad<O32>(k, l1, modeB, cc, bc.qb, ldsB)
+                                   : wall(stage_store(modeB, cc, stage_load<O32>(k, l1, bB, modeB, cc), ldsB));
+            bB.zero = bc.b.zero = z;
+        }
+        wave_lds_sync();
+    } else if (stA && stB) {
         const Tex4 tA = stage_load<O32>(k, l0, bA, modeA, cc);
         const Tex4 tB = stage_load<O32>(k, l1, bB, modeB, cc);
         const bool zA = stage_store(modeA, cc, tA, ldsA);
@@ -629,8 +805,10 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const bool readA = useA && !bA.zero, readB = useB && !bB.zero;
     if (useA) VCT_DBG(bA.zero ? 17 : 15);          // level-A samples from zero / nonzero bricks
     if (readA || readB) {
-        if (readA && active) sA = brick_sample<KL>(cA, bA, modeA != kFaces, bx, by, bz, wdx, wdy, wdz, ldsA);
-        if (readB && activeB) sB = brick_sample<KL>(cB, bB, modeB != kFaces, bx, by, bz, wdx, wdy, wdz, ldsB);
+        if (readA && active)
+            sA = brick_sample<KL>(cA, brick_slot(cA, bA, bc.qa), modeA != kFaces, bx, by, bz, wdx, wdy, wdz, ldsA);
+        if (readB && activeB)
+            sB = brick_sample<KL>(cB, brick_slot(cB, bB, bc.qb), modeB != kFaces, bx, by, bz, wdx, wdy, wdz, ldsB);
         wave_lds_sync();
     }
     pc.mark(3);
@@ -714,6 +892,35 @@ __device__ __forceinline__ bool spec_table(const TraceK& k, float tau, unsigned 
     return false;
 }
 
+// Ablation builds (perturbation measurements, never the product): extra work per
+// wave-step whose results are kept alive but never used, to measure how the
+// kernel time responds to more VALU / SALU issue (VCT_ABL_VALU / VCT_ABL_SALU =
+// instructions per wave-step).  VCT_ABL_GATHER / VCT_ABL_STAGE / VCT_ABL_LDS
+// issue every per-lane gather / staging load / LDS sample read twice.
+__device__ __forceinline__ void ablate_step(int i) {
+#if defined(VCT_ABL_VALU) && VCT_ABL_VALU > 0
+    float d0 = (float)i, d1 = d0, d2 = d0, d3 = d0;
+#pragma unroll
+    for (int j = 0; j < VCT_ABL_VALU / 4; ++j)
+        asm volatile("v_add_f32 %0, 1.0, %0\n v_add_f32 %1, 1.0, %1\n v_add_f32 %2, 1.0, %2\n v_add_f32 %3, 1.0, %3"
+                     : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+    asm volatile("" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3));
+#endif
+#if defined(VCT_ABL_SALU)
+    int s0 = i, s1 = i + 1;
+#pragma unroll
+    for (int j = 0; j < VCT_ABL_SALU / 2; ++j) asm volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1));
+    asm volatile("" ::"s"(s0), "s"(s1));
+#endif
+#if defined(VCT_ABL_NOP)
+#pragma unroll
+    for (int j = 0; j < VCT_ABL_NOP; ++j) asm volatile("s_nop 0");
+#endif
+#if defined(VCT_ABL_SLEEP)
+    __builtin_amdgcn_s_sleep(VCT_ABL_SLEEP);
+#endif
+}
+
 // one cone, wave-synchronous (A.6); same arithmetic as march().  TAB: (t, D,
 // l0, fr) come from a step table (the diffuse one, or a specular one).  CNT:
 // count steps and texel fetches (the launches that report them); else both stay 0.
@@ -759,8 +966,9 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.dir_uniform = wall_in(vm, (wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz)) && cc.nfaces == 3;
     }
     BrickCache bc;
-    bc.a = bc.b = BrickEntry{-1, 0, 0, 0, 0};
+    bc.a = bc.b = BrickEntry{-1, 0, 0, 0, 0, 0};
     bc.flip = 0;
+    bc.qa = bc.qb = 0u;
     for (int i = 0;; ++i) {
         float D, fr;
         int l0;
@@ -776,6 +984,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         active = active & (a < VCT_ALPHA_STOP) & (t <= k.tmax) & inside;
         const unsigned long long am = wballot(active);
         if (am == 0ull) break;
+        ablate_step(i);
         if constexpr (!TAB) {
             D = fmaxf(1.0f, tau2 * t);
             float m = spec_log2(D);
@@ -955,7 +1164,11 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
             }
         }
         dout = sel4(valid, make_float4(ir, ig, ib, 1.0f - occ), dout);
+#ifndef VCT_EXP_NOSPEC
         if (do_spec) {
+#else
+        if (false) {
+#endif
             float vx = k.ex - P.x, vy = k.ey - P.y, vz = k.ez - P.z;
             float vl = sqrtf(dot3(vx, vy, vz, vx, vy, vz));
             vl = valid ? vl : 1.0f;
@@ -1088,6 +1301,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.spec_state = c->spec_keys + kSpecSlots;
     k.spec_rows = c->spec_rows;
     k.spec_tabs = (a->variant & 0x100) ? 0 : 1;
+    k.abl0 = 0;
     // cone groups in separate workgroups (variant bits: 0x200 off, 0x400 three parts,
     // 0x800 two parts; default by launch size); per-pixel step counts need every
     // cone of a pixel in one lane, so steps_px keeps one part
@@ -1183,12 +1397,15 @@ extern "C" int vct_debug_waves(unsigned long long* out, int n) {   // out[n][3];
 }
 #endif
 #if defined(VCT_DEBUG_COUNTERS) || defined(VCT_DEBUG_CLOCK)
-extern "C" int vct_debug_counters(unsigned long long* out, int reset) {   // out[40]: 32 counters, 8 clocks
+extern "C" int vct_debug_counters(unsigned long long* out, int reset) {   // out[48]: 32 counters, 8 clocks, 8 more counters
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out + 40, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 8,
+                            sizeof(unsigned long long) * 32) != hipSuccess)
+        return -1;
     if (hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(vct_dbg_time), sizeof(unsigned long long) * 8) != hipSuccess)
         return -1;
     if (reset) {
-        unsigned long long z[32] = {};
+        unsigned long long z[40] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(vct_dbg_ctr), z, sizeof z) != hipSuccess) return -1;
         if (hipMemcpyToSymbol(HIP_SYMBOL(vct_dbg_time), z, sizeof(unsigned long long) * 8) != hipSuccess) return -1;
     }

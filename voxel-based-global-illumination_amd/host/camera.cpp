@@ -5,11 +5,18 @@
 
 namespace vcthost {
 
+// The float operation sequence of GLM as the reference calls it (bit-identical;
+// tests/test_ref_conventions.py checks every vector against the reference's own
+// camera.cpp + GLM, tests/golden/ref_camera.json):
+//  * glm::radians(d) = d * float(0.01745329251994329576923690768489)
+//    (glm/detail/func_trigonometric.inl:9-14);
+//  * glm::normalize(v) = v * (1 / sqrt(dot(v, v))), dot = (x x + y y) + z z
+//    (func_geometric.inl:48-55,82-90; func_exponential.inl:136-139).
 namespace {
-constexpr float kDeg = 3.14159265358979323846f / 180.0f;
+constexpr float kDeg = (float)0.01745329251994329576923690768489;
 void normalize(float v[3]) {
-    const float l = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-    v[0] /= l; v[1] /= l; v[2] /= l;
+    const float inv = 1.0f / std::sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+    v[0] *= inv; v[1] *= inv; v[2] *= inv;
 }
 void cross(const float a[3], const float b[3], float o[3]) {
     o[0] = a[1] * b[2] - a[2] * b[1];

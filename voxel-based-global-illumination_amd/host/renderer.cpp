@@ -52,7 +52,9 @@ bool ConeTraceRenderer::rebuild_scene() {
     std::vector<Vertex> v;
     std::vector<unsigned> idx, tri_mat;
     std::vector<float> kd4;
-    model->Flatten(v, idx, tri_mat, kd4);
+    Model placed = *model;              // the draw's model matrix, as the GL pass applies it (test.vert)
+    placed.Transform(s_.model);
+    placed.Flatten(v, idx, tri_mat, kd4);
     if (!check(vct_voxelize(ctx_, v.data(), sizeof(Vertex), (uint32_t)v.size(), idx.data(), (uint32_t)idx.size(),
                             tri_mat.data(), kd4.data(), (uint32_t)(kd4.size() / 4)), "vct_voxelize"))
         return false;

@@ -34,6 +34,9 @@ struct ConeTraceSettings {
     float aabb_min[3] = {-1.0f, -1.0f, -1.0f};
     float extent = 2.0f;
     uint32_t devices = 1;                 // > 1: one context over that many GPUs (vct_create_multi)
+    // model matrix applied to the model's vertices before K1, column-major; main.cpp
+    // sets the reference's T(0,-1.75,0) S(0.2) (r_voxelization.cpp:26-29) by default
+    float model[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
 };
 
 class ConeTraceRenderer : public Renderer {

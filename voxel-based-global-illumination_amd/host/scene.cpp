@@ -493,6 +493,40 @@ void Model::Transform(const float m[16]) {
         }
 }
 
+bool Model::Bounds(float lo[3], float hi[3]) const {
+    bool any = false;
+    for (const Mesh& me : meshes)
+        for (const Vertex& v : me.vertices) {
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = any ? std::min(lo[k], v.Position[k]) : v.Position[k];
+                hi[k] = any ? std::max(hi[k], v.Position[k]) : v.Position[k];
+            }
+            any = true;
+        }
+    return any;
+}
+
+void ReferenceModelMatrix(float m[16]) {
+    // glm::translate(mat4(1), t): column 3 = c0 t.x + c1 t.y + c2 t.z + c3 (matrix_transform.inl),
+    // then glm::scale(., s): columns 0..2 scaled
+    const float t[3] = {0.0f, -1.75f, 0.0f}, sc = 0.2f;
+    float r[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    for (int row = 0; row < 4; ++row)
+        r[12 + row] = ((r[row] * t[0] + r[4 + row] * t[1]) + r[8 + row] * t[2]) + r[12 + row];
+    for (int c = 0; c < 3; ++c)
+        for (int row = 0; row < 4; ++row) r[4 * c + row] = r[4 * c + row] * sc;
+    for (int i = 0; i < 16; ++i) m[i] = r[i];
+}
+
+void GridForBounds(const float lo[3], const float hi[3], uint32_t n, float aabb_min[3], float* extent) {
+    float e = 0.0f;
+    for (int k = 0; k < 3; ++k) e = std::max(e, hi[k] - lo[k]);
+    if (!(e > 0.0f)) e = 1.0f;
+    const float E = e * (float)n / (float)(n - 2);
+    for (int k = 0; k < 3; ++k) aabb_min[k] = 0.5f * (lo[k] + hi[k]) - 0.5f * E;
+    *extent = E;
+}
+
 void Model::Flatten(std::vector<Vertex>& v, std::vector<unsigned>& idx, std::vector<unsigned>& tri_mat,
                     std::vector<float>& kd4) const {
     v.clear(); idx.clear(); tri_mat.clear(); kd4.clear();

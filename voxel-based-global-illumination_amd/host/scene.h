@@ -10,6 +10,7 @@
 // (see scene.cpp for the assimp 3.3 rules it reproduces).
 #pragma once
 #include <array>
+#include <cstdint>
 #include <memory>
 #include <string>
 #include <vector>
@@ -46,12 +47,25 @@ public:
     // Wavefront OBJ (+ mtllib).  Returns false and fills `err` on failure.
     bool LoadObj(const std::string& path, std::string* err);
 
-    // Apply a 4x4 column-major model matrix (r_voxelization.cpp:26-29 style).
+    // Apply a 4x4 column-major model matrix (r_voxelization.cpp:26-29 style):
+    // p' = (m0 x + m4 y + m8 z + m12, ...), in that float order.
     void Transform(const float m[16]);
+
+    // Axis-aligned bounds of every vertex position (false when the model is empty).
+    bool Bounds(float lo[3], float hi[3]) const;
 
     // Flatten to the C-ABI arrays: vertices, indices, per-triangle material, Kd table.
     void Flatten(std::vector<Vertex>& v, std::vector<unsigned>& idx, std::vector<unsigned>& tri_mat,
                  std::vector<float>& kd4) const;
 };
+
+// The model matrix VoxelizationRenderer::Render draws with:
+// glm::scale(glm::translate(mat4(1), (0, -1.75, 0)), (0.2, 0.2, 0.2)), column-major
+// (r_voxelization.cpp:26-29; values pinned by tests/golden/ref_camera.json).
+void ReferenceModelMatrix(float m[16]);
+
+// Cubic grid around [lo, hi] with one voxel of padding on every side at resolution n:
+// edge E = max extent * n / (n - 2), min corner = centre - E / 2.
+void GridForBounds(const float lo[3], const float hi[3], uint32_t n, float aabb_min[3], float* extent);
 
 }  // namespace vcthost

@@ -3,6 +3,7 @@
 #include <new>
 
 #include "../../include/vct_host.h"
+#include "camera.h"
 #include "scene.h"
 
 struct vcth_model {
@@ -58,4 +59,46 @@ int vcth_material(const vcth_model* m, uint32_t i, const char** name, float ka[4
 
 void vcth_free(vcth_model* m) { delete m; }
 
+
+void vcth_transform(vcth_model* m, const float mat[16]) {
+    if (m && mat) m->m.Transform(mat);
+}
+
+int vcth_bounds(const vcth_model* m, float lo[3], float hi[3]) {
+    return (m && lo && hi && m->m.Bounds(lo, hi)) ? 0 : -1;
+}
+
+void vcth_reference_model_matrix(float mat[16]) {
+    if (mat) vcthost::ReferenceModelMatrix(mat);
+}
+
+void vcth_grid_for_bounds(const float lo[3], const float hi[3], uint32_t n, float aabb_min[3], float* extent) {
+    if (lo && hi && aabb_min && extent && n > 2) vcthost::GridForBounds(lo, hi, n, aabb_min, extent);
+}
+
+int vcth_camera_eval(const float init[5], const char* kinds, const float* a, const float* b, int n_ops, float out[15]) {
+    if (!init || !out || (n_ops > 0 && (!kinds || !a || !b))) return -1;
+    vcthost::Camera c(init[0], init[1], init[2], init[3], init[4]);
+    for (int i = 0; i < n_ops; ++i) {
+        switch (kinds[i]) {
+            case 'm': c.ProcessMouseMovement(a[i], b[i]); break;
+            case 's': c.ProcessMouseScroll(a[i]); break;
+            case 'f': c.ProcessKeyboard(vcthost::FORWARD, a[i]); break;
+            case 'b': c.ProcessKeyboard(vcthost::BACKWARD, a[i]); break;
+            case 'l': c.ProcessKeyboard(vcthost::LEFT, a[i]); break;
+            case 'r': c.ProcessKeyboard(vcthost::RIGHT, a[i]); break;
+            default: return -1;
+        }
+    }
+    for (int k = 0; k < 3; ++k) {
+        out[k] = c.Position[k];
+        out[3 + k] = c.Front[k];
+        out[6 + k] = c.Right[k];
+        out[9 + k] = c.Up[k];
+    }
+    out[12] = c.Yaw;
+    out[13] = c.Pitch;
+    out[14] = c.Zoom;
+    return 0;
+}
 }  // extern "C"

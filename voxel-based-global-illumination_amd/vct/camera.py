@@ -43,6 +43,16 @@ class Camera:
             self.pitch = max(-89.0, min(89.0, self.pitch))
         self._update()
 
+    def process_scroll(self, dy: float):  # camera.cpp:63-71
+        if 1.0 <= self.zoom <= 45.0:
+            self.zoom -= dy
+        self.zoom = min(45.0, max(1.0, self.zoom))
+
+    def process_keyboard(self, direction: str, dt: float):  # camera.cpp:29-40
+        v = SPEED * dt
+        step = {"FORWARD": self.front, "BACKWARD": -self.front, "LEFT": -self.right, "RIGHT": self.right}[direction]
+        self.position = self.position + step * v
+
     def view_matrix(self) -> np.ndarray:
         """glm::lookAtRH(Position, Position + Front, Up) (camera.cpp:26)."""
         f, s, u = self.front, self.right, np.cross(self.right, self.front)
@@ -68,3 +78,16 @@ class Camera:
         c.right[:] = [float(x) for x in self.right]
         c.zoom_deg, c.near_plane, c.far_plane = self.zoom, self.near, self.far
         return c
+
+
+def reference_model_matrix() -> np.ndarray:
+    """The model matrix of VoxelizationRenderer::Render, column-major float32:
+    glm::scale(glm::translate(mat4(1), (0, -1.75, 0)), (0.2, 0.2, 0.2))
+    (r_voxelization.cpp:26-29), in GLM's float operation order."""
+    m = np.eye(4, dtype=np.float32).T.reshape(-1).copy()        # column-major identity
+    t = np.array([0.0, -1.75, 0.0], np.float32)
+    for row in range(4):                                         # translate: col3 = c0 tx + c1 ty + c2 tz + c3
+        m[12 + row] = ((m[row] * t[0] + m[4 + row] * t[1]) + m[8 + row] * t[2]) + m[12 + row]
+    m[:12] = m[:12] * np.float32(0.2)                            # scale: columns 0..2
+    return m
+
