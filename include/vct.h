@@ -20,8 +20,9 @@
  *  - Host-pointer entry points are synchronous on return.  *_device entry
  *    points take device pointers and are asynchronous on the ctx stream
  *    (vct_set_stream); vct_synchronize() waits for them.
- *  - Data layouts: grids are linear-Z RGBA32F, index x + n*(y + n*z); the
- *    G-buffer and outputs are [h][w][4] float, row 0 = top of the image.
+ *  - Data layouts: grids cross the ABI linear-Z RGBA32F, index x + n*(y + n*z)
+ *    (the device copy is bricked, see vct_level0_device); the G-buffer and
+ *    outputs are [h][w][4] float, row 0 = top of the image.
  *  - Semantics: SURVEY.md Appendix A with the literals of vct_spec.h.
  */
 #ifndef VCT_H
@@ -247,7 +248,12 @@ vct_status vct_level_dims(const vct_ctx* ctx, uint32_t level, uint32_t* n_l, uin
 vct_status vct_download_level(vct_ctx* ctx, uint32_t level, uint32_t face, float* host_rgba);
 /* replaces the level-0 radiance grid (n^3 x 4 floats, host) */
 vct_status vct_upload_level0(vct_ctx* ctx, const float* host_rgba);
-/* device pointer + size of the level-0 radiance grid (RCCL broadcast buffer) */
+/* device pointer + size of the level-0 radiance grid (RCCL broadcast buffer).
+ * Device-side level 0 is in the library's internal texel layout (2x2x2 bricks of
+ * 8 texels, bricks in linear-Z order; vct_device.h texel_index), not linear-Z:
+ * the device pointer and the two device copies below are for moving level 0
+ * between contexts of this library (broadcast, replication), not for reading
+ * texels; vct_download_level / vct_upload_level0 convert to / from linear-Z. */
 vct_status vct_level0_device(vct_ctx* ctx, void** dptr, size_t* bytes);
 /* device-to-device copies of the level-0 grid on the ctx stream (host RCCL
  * glue that owns its own communication buffer, e.g. a torch tensor) */

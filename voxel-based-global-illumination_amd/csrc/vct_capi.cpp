@@ -657,7 +657,11 @@ vct_status vct_download_level(vct_ctx* c, uint32_t level, uint32_t face, float* 
     if (st != VCT_OK) return st;
     const size_t nl = c->grid.n >> level, vl = nl * nl * nl;
     const float4* src = c->grid.pyr + c->grid.lvl_off[level] + face * vl;
-    VCT_HIP(hipMemcpyAsync(host, src, vl * 16, hipMemcpyDeviceToHost, c->stream), "download level");
+    // the ABI's layout is linear-Z; the pyramid's is vct_device.h's texel layout
+    void* tmp;
+    VCT_HIP(scratch_get(c, 0, vl * 16, &tmp), "scratch");
+    VCT_HIP(launch_relayout(c, src, (float4*)tmp, (uint32_t)nl, true), "relayout");
+    VCT_HIP(hipMemcpyAsync(host, tmp, vl * 16, hipMemcpyDeviceToHost, c->stream), "download level");
     VCT_HIP(hipStreamSynchronize(c->stream), "sync");
     return VCT_OK;
 }
@@ -667,7 +671,10 @@ vct_status vct_upload_level0(vct_ctx* c, const float* host) {
     vct_status st = use_device(c);
     if (st != VCT_OK) return st;
     const size_t nv = (size_t)c->grid.n * c->grid.n * c->grid.n;
-    VCT_HIP(hipMemcpyAsync(c->grid.pyr, host, nv * 16, hipMemcpyHostToDevice, c->stream), "upload level0");
+    void* tmp;
+    VCT_HIP(scratch_get(c, 0, nv * 16, &tmp), "scratch");
+    VCT_HIP(hipMemcpyAsync(tmp, host, nv * 16, hipMemcpyHostToDevice, c->stream), "upload level0");
+    VCT_HIP(launch_relayout(c, (const float4*)tmp, c->grid.pyr, c->grid.n, false), "relayout");
     VCT_HIP(hipStreamSynchronize(c->stream), "sync");
     c->grid.injected = true;
     c->grid.l0_dense = true;

@@ -81,6 +81,8 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts,
 hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb);
 // K3
 hipError_t launch_mips(vct_ctx* c);
+// one nl^3 face volume between the pyramid's texel layout and linear-Z (vct_device.h)
+hipError_t launch_relayout(vct_ctx* c, const float4* src, float4* dst, uint32_t nl, bool to_linear);
 // K4
 hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a);
 hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t planes, uint32_t w, uint32_t h,

@@ -264,6 +264,26 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
     uint32_t idx[8];
     bool in[8];
     const int xs[2] = {ix, ix + 1}, ys[2] = {iy, iy + 1}, zs[2] = {iz, iz + 1};
+#if VCT_BRICK2
+    // brick layout (vct_device.h texel_index), per-axis terms: corner index = X + Y + Z.
+    // 24-bit multiplies (v_mul_lo_u32 is quarter rate) where every in-range term fits
+    // (n <= 512: (z >> 1) nb^2 < 2^24); an out-of-range corner's index is never read
+    const uint32_t nb = nl > 1 ? (uint32_t)nl >> 1 : 1u, nb2 = nb * nb;
+    uint32_t tx[2], ty[2], tz[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t x = (uint32_t)xs[j], y = (uint32_t)ys[j], z = (uint32_t)zs[j];
+        tx[j] = ((x >> 1) << 3) | (x & 1u);
+        ty[j] = ((O32 ? __umul24(y >> 1, nb) : (y >> 1) * nb) << 3) | ((y & 1u) << 1);
+        tz[j] = ((O32 ? __umul24(z >> 1, nb2) : (z >> 1) * nb2) << 3) | ((z & 1u) << 2);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int x = xs[c & 1], y = ys[(c >> 1) & 1], z = zs[c >> 2];
+        in[c] = (unsigned)x < (unsigned)nl && (unsigned)y < (unsigned)nl && (unsigned)z < (unsigned)nl;
+        idx[c] = tx[c & 1] + ty[(c >> 1) & 1] + tz[c >> 2];
+    }
+#else
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         const int x = xs[c & 1], y = ys[(c >> 1) & 1], z = zs[c >> 2];
@@ -272,6 +292,7 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
         // for every in-range corner; an out-of-range corner's index is never read (in[c] = false)
         idx[c] = (uint32_t)x + __umul24((uint32_t)nl, (uint32_t)y + __umul24((uint32_t)nl, (uint32_t)z));
     }
+#endif
     const auto lv = [&] {
         if constexpr (UNIF) return level_view<O32>(k, l);
         else return level_view_lane(k, l);
@@ -530,7 +551,7 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
     const int lane = threadIdx.x & 63;
     const int sx = be.ox + (lane & 3), sy = be.oy + ((lane >> 2) & 3), sz = be.oz + (lane >> 4);
     const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
-    const uint32_t gi = (uint32_t)sx + __umul24((uint32_t)nl, (uint32_t)sy + __umul24((uint32_t)nl, (uint32_t)sz));
+    const uint32_t gi = texel_index((uint32_t)sx, (uint32_t)sy, (uint32_t)sz, (uint32_t)nl);
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const LevelView<O32> lv = level_view<O32>(k, l);
     Tex4 t;
@@ -605,7 +626,7 @@ __device__ __forceinline__ bool stage_quad(const TraceK& k, int l, int mode, con
             const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)qo, 16 * (h + i));
             const int sx = qo_x(q) + tx, sy = qo_y(q) + ty, sz = qo_z(q) + tz;
             const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
-            const uint32_t gi = (uint32_t)sx + __umul24((uint32_t)nl, (uint32_t)sy + __umul24((uint32_t)nl, (uint32_t)sz));
+            const uint32_t gi = texel_index((uint32_t)sx, (uint32_t)sy, (uint32_t)sz, (uint32_t)nl);
             if (mode == kIso) {
                 v[i] = lv.fetch(gi, inb);
             } else {

@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__
 // One lane per listed voxel (grid-stride, the count is on the device).
 __global__ void __launch_bounds__(256) k1_clear(const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list,
                                                 long long* __restrict__ accum, float4* __restrict__ albedo_occ,
-                                                float4* __restrict__ normal, float4* __restrict__ level0) {
+                                                float4* __restrict__ normal, float4* __restrict__ level0, uint32_t n) {
     const uint32_t cnt = *n_list;
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const longlong2 z = make_longlong2(0, 0);
@@ -295,7 +295,7 @@ __global__ void __launch_bounds__(256) k1_clear(const uint32_t* __restrict__ lis
         a[0] = z; a[1] = z; a[2] = z; a[3] = z;
         albedo_occ[v] = z4;
         normal[v] = z4;
-        level0[v] = z4;                          // K2 wrote only occupied voxels
+        level0[l0_texel((uint32_t)v, n)] = z4;   // K2 wrote only occupied voxels
     }
 }
 
@@ -398,7 +398,7 @@ constexpr int kShadeJ = 16;
 __global__ void __launch_bounds__(256) k2_shade(const uint32_t* __restrict__ occ, const uint32_t* __restrict__ n_occ,
                                                 const float4* __restrict__ normal, float lx, float ly, float lz,
                                                 uint32_t* __restrict__ lit, uint32_t* __restrict__ n_lit,
-                                                float4* __restrict__ r0) {
+                                                float4* __restrict__ r0, uint32_t n) {
     __shared__ uint32_t s_cnt[kShadeJ * 4];
     __shared__ uint32_t s_base;
     const uint32_t cnt = *n_occ;
@@ -414,7 +414,7 @@ __global__ void __launch_bounds__(256) k2_shade(const uint32_t* __restrict__ occ
                 const float4 nm = normal[v];
                 const float ndl = dot3(nm.x, nm.y, nm.z, lx, ly, lz);
                 if (ndl > 0.0f) flags |= 1u << j;
-                else r0[v] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+                else r0[l0_texel(v, n)] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
                 vs[j] = v;
             }
             const unsigned long long b = __ballot((flags >> j) & 1u);
@@ -550,7 +550,8 @@ __global__ void __launch_bounds__(1024) k2_walk(const uint32_t* __restrict__ lit
                   z = (int)(v / ((uint32_t)n * (uint32_t)n));
         const float vis = dda_coarse(bits, cbits, n, cs, cn, ((float)x + 0.5f) + nm.x, ((float)y + 0.5f) + nm.y,
                                      ((float)z + 0.5f) + nm.z, lx, ly, lz);
-        r0[v] = make_float4(((ao.x * cr) * ndl) * vis, ((ao.y * cg) * ndl) * vis, ((ao.z * cb) * ndl) * vis, 1.0f);
+        r0[l0_texel(v, (uint32_t)n)] =
+            make_float4(((ao.x * cr) * ndl) * vis, ((ao.y * cg) * ndl) * vis, ((ao.z * cb) * ndl) * vis, 1.0f);
     }
 }
 
@@ -564,7 +565,8 @@ __global__ void __launch_bounds__(256) k2_inject(const float4* __restrict__ albe
     size_t nv = (size_t)n * n * n;
     if (v >= nv) return;
     float4 ao = albedo_occ[v];
-    if (ao.w == 0.0f) { r0[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f); return; }
+    float4* const dst = r0 + l0_texel((uint32_t)v, (uint32_t)n);
+    if (ao.w == 0.0f) { *dst = make_float4(0.0f, 0.0f, 0.0f, 0.0f); return; }
     float4 nm = normal[v];
     float ndl = dot3(nm.x, nm.y, nm.z, lx, ly, lz);
     float4 out = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
@@ -576,7 +578,7 @@ __global__ void __launch_bounds__(256) k2_inject(const float4* __restrict__ albe
         out.y = ((ao.y * cg) * ndl) * vis;
         out.z = ((ao.z * cb) * ndl) * vis;
     }
-    r0[v] = out;
+    *dst = out;
 }
 
 }  // namespace
@@ -611,7 +613,7 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
     const size_t nwords = nv / 64;
     const uint32_t lb = (uint32_t)std::min<size_t>((nv + 255) / 256, 4096);
     hipLaunchKernelGGL(k1_clear, dim3(lb), dim3(256), 0, s, g.occ_list, g.occ_count, g.accum, g.albedo_occ,
-                       g.normal, g.pyr);
+                       g.normal, g.pyr, g.n);
     if ((e = hipMemsetAsync(g.occ_bits, 0, nwords * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(g.occ_count, 0, 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(total, 0, 8, s)) != hipSuccess) return e;
@@ -681,7 +683,7 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
                        coarse);
     const uint32_t blocks = (uint32_t)std::min<size_t>((nv / 64 + 255) / 256 + 1, 4096);
     hipLaunchKernelGGL(k2_shade, dim3(blocks), dim3(256), 0, s, g.occ_list, g.occ_count, g.normal, lx, ly, lz, lit,
-                       counts, g.pyr);
+                       counts, g.pyr, g.n);
     hipLaunchKernelGGL(k2_walk, dim3(512), dim3(1024), 0, s, lit, counts, coarse, cs,
                        g.albedo_occ, g.normal, g.occ_bits, (int)g.n, lx, ly, lz, cr, cg, cb, g.pyr);
     return hipGetLastError();
