@@ -14,7 +14,8 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "voxel-based-global-illumination_amd")
-os.environ["VCT_LIB"] = os.path.join(PKG, "vct", "libvct_hip_clk.so" if "--clk" in sys.argv else "libvct_hip_dbg.so")
+os.environ["VCT_LIB"] = os.environ.get("VCT_DBG_LIB") or os.path.join(
+    PKG, "vct", "libvct_hip_clk.so" if "--clk" in sys.argv else "libvct_hip_dbg.so")
 sys.path[:0] = [REPO, PKG]
 
 

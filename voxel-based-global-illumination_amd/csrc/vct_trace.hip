@@ -111,6 +111,7 @@ struct TraceK {
     const float4* pyr;
     uint64_t lvl_off[kMaxLevels + 1];
     int n, L;
+    int lgn;                     // log2 n
     float g0x, g0y, g0z, inv_h, tmax;
     const float4* pos;
     const float4* nrm;
@@ -248,12 +249,85 @@ __device__ __forceinline__ LevelView<false> level_view_lane(const TraceK& k, int
 // ===========================================================================
 // per-lane gathers (variant 1, and the fallback of variant 0)
 // ===========================================================================
+// Brick layout byte offsets as OR-able bit fields (n a power of two): inside a face
+// volume of nl^3 texels, coordinate x contributes (x >> 1) << 7 | (x & 1) << 4, y
+// (y >> 1) << (lnb + 7) | (y & 1) << 5 and z (z >> 1) << (2 lnb + 7) | (z & 1) << 6
+// (nb = nl / 2 = 2^lnb bricks per axis); face f adds f << (3 lg nl + 4).  The fields
+// are disjoint, so a texel's byte offset is the OR of its three axis terms (and its
+// face), and an axis term of kOut = 0xfffffff0 for a coordinate outside the level
+// makes the OR kOut: past the buffer resource's range, which reads as 0 (the spec's
+// zero border).  One v_or3 per corner instead of adds, range checks and selects.
+constexpr uint32_t kOut = 0xfffffff0u;
+struct AxisTerms { uint32_t t0, t1; };     // coordinates c and c + 1
+__device__ __forceinline__ AxisTerms axis_terms(int c, uint32_t nl, uint32_t sh, uint32_t bit) {
+    const uint32_t u = (uint32_t)c, odd = u & 1u;
+    const uint32_t t0 = ((u >> 1) << sh) | (odd << bit);
+    // c + 1: the same 2-brick when c is even (+ 1 << bit), else the next one (wraps to 0 for c = -1)
+    const uint32_t t1 = odd ? t0 + ((1u << sh) - (1u << bit)) : t0 + (1u << bit);
+    return AxisTerms{u < nl ? t0 : kOut, u + 1u < nl ? t1 : kOut};
+}
+
+struct LevelBits { uint32_t nl, shy, shz, shf; };   // per level l (wave-uniform)
+__device__ __forceinline__ LevelBits level_bits(const TraceK& k, int l) {
+    const uint32_t lg = (uint32_t)(k.lgn - l), lnb = lg > 0u ? lg - 1u : 0u;
+    return LevelBits{1u << lg, lnb + 7u, 2u * lnb + 7u, 3u * lg + 4u};
+}
+
+// D_l for a wave-uniform level through its buffer resource (O32, brick layout):
+// same texels, weights and fmaf order as sample_level
+__device__ __forceinline__ float4 sample_level_bits(const TraceK& k, int l, float qx, float qy, float qz, int fx,
+                                                    int fy, int fz, float wdx, float wdy, float wdz) {
+    const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
+    const float cx = qx * scale - 0.5f, cy = qy * scale - 0.5f, cz = qz * scale - 0.5f;
+    const float flx = floorf(cx), fly = floorf(cy), flz = floorf(cz);
+    float wc[8];
+    corner_weights(cx - flx, cy - fly, cz - flz, wc);
+    const LevelBits lb = level_bits(k, l);
+    const AxisTerms X = axis_terms((int)flx, lb.nl, 7u, 4u), Y = axis_terms((int)fly, lb.nl, lb.shy, 5u),
+                    Z = axis_terms((int)flz, lb.nl, lb.shz, 6u);
+    uint32_t off[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) off[c] = (c & 1 ? X.t1 : X.t0) | ((c >> 1) & 1 ? Y.t1 : Y.t0) | (c >> 2 ? Z.t1 : Z.t0);
+    const LevelView<true> lv = level_view<true>(k, l);
+    const auto ld = [&](uint32_t o) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(lv.r, o, 0, 0);
+        return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    };
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (l == 0 || !k.aniso) {
+        float4 v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = ld(off[c]);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc_fma(acc, wc[c], v[c]);
+        return acc;
+    }
+    const uint32_t FX = (uint32_t)fx << lb.shf, FY = (uint32_t)fy << lb.shf, FZ = (uint32_t)fz << lb.shf;
+#pragma unroll
+    for (int h = 0; h < 8; h += kCh) {         // kCh corners x 3 faces in flight
+        float4 vx[kCh], vy[kCh], vz[kCh];
+#pragma unroll
+        for (int c = 0; c < kCh; ++c) {
+            vx[c] = ld(off[h + c] | FX);
+            vy[c] = ld(off[h + c] | FY);
+            vz[c] = ld(off[h + c] | FZ);
+        }
+#pragma unroll
+        for (int c = 0; c < kCh; ++c) acc_fma(acc, wc[h + c], combine3(wdx, wdy, wdz, vx[c], vy[c], vz[c]));
+        __builtin_amdgcn_sched_barrier(0);     // keep the next chunk's loads below (VGPR budget)
+    }
+    return acc;
+}
+
 // D_l(q, d) (A.5): level 0 / isotropic = T_l; anisotropic = faces combined per
 // corner texel, then trilinear.  Zero border: out-of-range corners read as 0
 // (LevelView); fmaf(w, 0, acc) == acc, the spec's zero-border sum.
 template <bool O32, bool UNIF = false>   // UNIF: l is wave-uniform (buffer resource); else per lane
 __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx, float qy, float qz,
                                                int fx, int fy, int fz, float wdx, float wdy, float wdz) {
+#if VCT_BRICK2 && !defined(VCT_ABL_GATHER)
+    if constexpr (O32 && UNIF) return sample_level_bits(k, l, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+#endif
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
     const int nl = k.n >> l;
     const float cx = qx * scale - 0.5f, cy = qy * scale - 0.5f, cz = qz * scale - 0.5f;
@@ -1300,6 +1374,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.pyr = g.pyr;
     for (int i = 0; i <= kMaxLevels; ++i) k.lvl_off[i] = g.lvl_off[i];
     k.n = (int)g.n; k.L = (int)g.L;
+    k.lgn = __builtin_ctz(g.n);
     k.g0x = g.g0[0]; k.g0y = g.g0[1]; k.g0z = g.g0[2];
     k.inv_h = g.inv_h;
     k.tmax = (float)g.n * VCT_SQRT3;
