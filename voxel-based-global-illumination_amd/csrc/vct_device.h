@@ -63,6 +63,18 @@ __host__ __device__ __forceinline__ uint32_t texel_index(uint32_t x, uint32_t y,
 #endif
 }
 
+// texel_index for nl = 2^lg from shifts: the same value for every in-range texel
+// (x >> 1 < nb); out-of-range coordinates give an unspecified index (never read)
+__host__ __device__ __forceinline__ uint32_t texel_index_lg(uint32_t x, uint32_t y, uint32_t z, uint32_t lg) {
+#if VCT_BRICK2
+    const uint32_t lnb = lg > 0u ? lg - 1u : 0u;
+    return (((x >> 1) | ((y >> 1) << lnb) | ((z >> 1) << (2u * lnb))) << 3) | ((z & 1u) << 2) | ((y & 1u) << 1) |
+           (x & 1u);
+#else
+    return x + ((y + (z << lg)) << lg);
+#endif
+}
+
 // inverse of texel_index: (x, y, z) of index v in a face volume of nl^3 texels
 __host__ __device__ __forceinline__ void texel_coords(uint32_t v, uint32_t nl, uint32_t& x, uint32_t& y, uint32_t& z) {
 #if VCT_BRICK2

@@ -50,8 +50,10 @@ __device__ unsigned long long vct_dbg_wave[kDbgWaves][3];   // start, end, HW_ID
 #endif
 #ifdef VCT_DEBUG_COUNTERS
 #define VCT_DBG(i) do { if ((threadIdx.x & 63) == 0) atomicAdd(&vct_dbg_ctr[i], 1ull); } while (0)
+#define VCT_DBGN(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&vct_dbg_ctr[i], (unsigned long long)(v)); } while (0)
 #else
 #define VCT_DBG(i) do { } while (0)
+#define VCT_DBGN(i, v) do { } while (0)
 #endif
 
 // Clock-build (make clk -> vct/libvct_hip_clk.so) per-wave phase clock
@@ -94,6 +96,13 @@ struct PhaseClock {
 };
 
 extern "C" __device__ int __ockl_wfred_min_i32(int);   // wave-wide min over the active lanes
+
+// c = q 2^-l - 1/2 as one fma: the product by a power of two is exact (no overflow,
+// and an underflowed product is absorbed by the - 1/2), so the fused form rounds once
+// where the spec rounds once: bit-identical
+__device__ __forceinline__ float lvl_coord(float q, float scale) {
+    return fmaf(q, scale, -0.5f);
+}
 
 #ifndef VCT_K4_MIN_WAVES
 #define VCT_K4_MIN_WAVES 4      // __launch_bounds__ minimum waves per SIMD of K4 (128 VGPRs)
@@ -278,7 +287,7 @@ __device__ __forceinline__ LevelBits level_bits(const TraceK& k, int l) {
 __device__ __forceinline__ float4 sample_level_bits(const TraceK& k, int l, float qx, float qy, float qz, int fx,
                                                     int fy, int fz, float wdx, float wdy, float wdz) {
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
-    const float cx = qx * scale - 0.5f, cy = qy * scale - 0.5f, cz = qz * scale - 0.5f;
+    const float cx = lvl_coord(qx, scale), cy = lvl_coord(qy, scale), cz = lvl_coord(qz, scale);
     const float flx = floorf(cx), fly = floorf(cy), flz = floorf(cz);
     float wc[8];
     corner_weights(cx - flx, cy - fly, cz - flz, wc);
@@ -290,6 +299,14 @@ __device__ __forceinline__ float4 sample_level_bits(const TraceK& k, int l, floa
     for (int c = 0; c < 8; ++c) off[c] = (c & 1 ? X.t1 : X.t0) | ((c >> 1) & 1 ? Y.t1 : Y.t0) | (c >> 2 ? Z.t1 : Z.t0);
     const LevelView<true> lv = level_view<true>(k, l);
     const auto ld = [&](uint32_t o) {
+#ifdef VCT_ABL_GATHER
+        // ablation: the same load again (soffset = an opaque 0), its value kept alive unused;
+        // VCT_ABL_GATHER = 1 every lane, 2 one lane of each 2x2 pixel quad, 3 the first 16 lanes
+        if (VCT_ABL_GATHER == 1 || (VCT_ABL_GATHER == 2 ? (threadIdx.x & 3) == 0 : (threadIdx.x & 63) < 16)) {
+            const auto w = __builtin_amdgcn_raw_buffer_load_b128(lv.r, o, k.abl0, 0);
+            asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
+        }
+#endif
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(lv.r, o, 0, 0);
         return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
     };
@@ -325,12 +342,12 @@ __device__ __forceinline__ float4 sample_level_bits(const TraceK& k, int l, floa
 template <bool O32, bool UNIF = false>   // UNIF: l is wave-uniform (buffer resource); else per lane
 __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx, float qy, float qz,
                                                int fx, int fy, int fz, float wdx, float wdy, float wdz) {
-#if VCT_BRICK2 && !defined(VCT_ABL_GATHER)
+#if VCT_BRICK2
     if constexpr (O32 && UNIF) return sample_level_bits(k, l, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
 #endif
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
     const int nl = k.n >> l;
-    const float cx = qx * scale - 0.5f, cy = qy * scale - 0.5f, cz = qz * scale - 0.5f;
+    const float cx = lvl_coord(qx, scale), cy = lvl_coord(qy, scale), cz = lvl_coord(qz, scale);
     const float flx = floorf(cx), fly = floorf(cy), flz = floorf(cz);
     const int ix = (int)flx, iy = (int)fly, iz = (int)flz;
     float wc[8];
@@ -530,7 +547,7 @@ struct Corner {                  // one lane's trilinear footprint at one level
 
 __device__ __forceinline__ Corner level_corner(int l, float qx, float qy, float qz) {
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);   // 2^-l, exact
-    const float cx = qx * scale - 0.5f, cy = qy * scale - 0.5f, cz = qz * scale - 0.5f;
+    const float cx = lvl_coord(qx, scale), cy = lvl_coord(qy, scale), cz = lvl_coord(qz, scale);
     const float flx = floorf(cx), fly = floorf(cy), flz = floorf(cz);
     Corner c;
     c.fx = cx - flx; c.fy = cy - fly; c.fz = cz - flz;
@@ -548,12 +565,23 @@ __device__ __forceinline__ bool in_brick(const Corner& c, const BrickEntry& b) {
 // brick's slack (3 - span corners) is put ahead of the march: origin = min
 // when the cone moves toward +axis, max - 2 when it moves toward -axis (neg),
 // so the following steps stay inside longer.
-__device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl, bool neg) {
+// negb = 0 or 1 (the cone moves toward -axis): integer arithmetic on wave-uniform values
+// only, so the origin stays on the scalar unit (a `neg ? :` on a bool is lowered as a
+// lane mask and drags the origin into VGPRs)
+// (m != 0) as an SGPR integer: LLVM lowers a uniform i1 to a lane mask and would
+// finish the origin arithmetic on the VALU (v_cndmask / v_addc / v_mul_lo)
+__device__ __forceinline__ int s_nonzero(unsigned long long m) {
+    int r;
+    asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(m) : "scc");
+    return r;
+}
+__device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl, int negb) {
     const int b = __builtin_amdgcn_readlane(v, fl);
-    const int d = neg ? b - v : v - b;
-    const unsigned long long m2 = wballot(d < -1) & am, m1 = wballot(d < 0) & am;   // m2 within m1
-    const int cnt = (int)(m1 != 0ull) + (int)(m2 != 0ull);
-    return neg ? b + cnt - 2 : b - cnt;
+    const int sg = 1 - 2 * negb;                       // +1 / -1
+    const int sv = __mul24(v, sg), sb = b * sg;        // mirrored toward -axis
+    const unsigned long long m2 = wballot(sv < sb - 1) & am, m1 = wballot(sv < sb) & am;   // m2 within m1
+    const int cnt = s_nonzero(m1) + s_nonzero(m2);
+    return b - sg * cnt - 2 * negb;
 }
 
 // a brick origin over the lanes of am (neg: bit a = the cone moves toward -axis a),
@@ -561,8 +589,8 @@ __device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl,
 __device__ __forceinline__ bool brick_origin(const Corner& c, unsigned long long am, int neg, BrickEntry& b) {
     const int fl = am ? __builtin_ctzll(am) : 0;
     b.ox = wave_origin(c.ix, am, fl, neg & 1);
-    b.oy = wave_origin(c.iy, am, fl, neg & 2);
-    b.oz = wave_origin(c.iz, am, fl, neg & 4);
+    b.oy = wave_origin(c.iy, am, fl, (neg >> 1) & 1);
+    b.oz = wave_origin(c.iz, am, fl, (neg >> 2) & 1);
     return wall_in(am, in_brick(c, b));
 }
 
@@ -625,7 +653,7 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
     const int lane = threadIdx.x & 63;
     const int sx = be.ox + (lane & 3), sy = be.oy + ((lane >> 2) & 3), sz = be.oz + (lane >> 4);
     const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
-    const uint32_t gi = texel_index((uint32_t)sx, (uint32_t)sy, (uint32_t)sz, (uint32_t)nl);
+    const uint32_t gi = texel_index_lg((uint32_t)sx, (uint32_t)sy, (uint32_t)sz, (uint32_t)(k.lgn - l));
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const LevelView<O32> lv = level_view<O32>(k, l);
     Tex4 t;
@@ -992,6 +1020,11 @@ __device__ __forceinline__ bool spec_table(const TraceK& k, float tau, unsigned 
 // kernel time responds to more VALU / SALU issue (VCT_ABL_VALU / VCT_ABL_SALU =
 // instructions per wave-step).  VCT_ABL_GATHER / VCT_ABL_STAGE / VCT_ABL_LDS
 // issue every per-lane gather / staging load / LDS sample read twice.
+__device__ __forceinline__ int vct_abl_zero() {
+    int z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    return z;
+}
 __device__ __forceinline__ void ablate_step(int i) {
 #if defined(VCT_ABL_VALU) && VCT_ABL_VALU > 0
     float d0 = (float)i, d1 = d0, d2 = d0, d3 = d0;
@@ -1002,7 +1035,8 @@ __device__ __forceinline__ void ablate_step(int i) {
     asm volatile("" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3));
 #endif
 #if defined(VCT_ABL_SALU)
-    int s0 = i, s1 = i + 1;
+    (void)i;
+    int s0 = __builtin_amdgcn_readfirstlane(vct_abl_zero()), s1 = s0 + 3;   // not tied to the loop counter
 #pragma unroll
     for (int j = 0; j < VCT_ABL_SALU / 2; ++j) asm volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1));
     asm volatile("" ::"s"(s0), "s"(s1));
@@ -1075,10 +1109,13 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         }
         const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
         // a >= 0.95, t > tmax or outside the grid ends the lane's march (no short-circuit branches)
-        const bool inside = (qx >= 0.0f) & (qx <= nf) & (qy >= 0.0f) & (qy <= nf) & (qz >= 0.0f) & (qz <= nf);
+        const bool inside = (fminf(fminf(qx, qy), qz) >= 0.0f) & (fmaxf(fmaxf(qx, qy), qz) <= nf);
         active = active & (a < VCT_ALPHA_STOP) & (t <= k.tmax) & inside;
         const unsigned long long am = wballot(active);
         if (am == 0ull) break;
+        VCT_DBG(TAB ? 36 : 38);                               // wave-steps (table / per-lane steps)
+        VCT_DBGN(37, __builtin_popcountll(am));               // active lanes over those wave-steps
+        VCT_DBGN(39, __builtin_popcountll(wballot(valid)));   // lanes holding a valid pixel
         ablate_step(i);
         if constexpr (!TAB) {
             D = fmaxf(1.0f, tau2 * t);
