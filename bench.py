@@ -82,7 +82,9 @@ def parse():
     p.add_argument("--gbuffer", default="scene", choices=["scene", "rand"])
     p.add_argument("--n-diffuse", type=int, default=9)
     p.add_argument("--no-spec", action="store_true")
-    p.add_argument("--variant", type=int, default=0)
+    p.add_argument("--variant", type=lambda v: int(v, 0), default=0)
+    p.add_argument("--reorder", action="store_true",
+                   help="ray reordering (variant bit 0x8000): pixels traced in Morton order of their origin voxel")
     p.add_argument("--exchange", default="present", choices=["present", "allgather"],
                    help="N > 1: assemble the frame on rank 0 (send/recv) or on every rank (all-gather)")
     p.add_argument("--secondary", default="courtyard",
@@ -91,7 +93,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-json", default=PROFILE)
     p.add_argument("--dry-run", action="store_true", help="CPU rehearsal of the rank plumbing (gloo), no GPU")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.reorder:
+        a.variant |= 0x8000
+    return a
 
 
 # ---------------------------------------------------------------------------

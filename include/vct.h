@@ -93,7 +93,10 @@ typedef struct vct_trace_args {
                               the four-face union, 3 row-major lanes; flags: 0x100 no
                               specular step tables, 0x200 all cones in one workgroup,
                               0x400 / 0x800 three / two cone parts, 0x1000 four waves
-                              per workgroup, 0x4000 the counting form without counters;
+                              per workgroup, 0x4000 the counting form without counters,
+                              0x8000 ray reordering: pixels traced in the order of the Morton
+                              code of their cone origin's voxel (for incoherent G-buffers such
+                              as G_rand; one-rank full frames only, ignored otherwise);
                               bits 20-23: diffuse parts of the three-part split (2 default)
                                                                   */
 } vct_trace_args;

@@ -141,7 +141,8 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     gb = [torch.from_numpy(a).to(dev) for a in (pos, nrm, alb)]
     ref = O.trace(n, g0, E, ctx.download_level(0), gpu_pyramid_flat(ctx), pos, nrm, alb, cam.position)
-    for variant in (0, 1, 2, 3):
+    # 0x8000: rays reordered by the Morton code of their origin voxel (alone, with gathers, without the union)
+    for variant in (0, 1, 2, 3, 0x8000, 0x8001, 0x8002):
         d = torch.empty((h, w, 4), device=dev)
         sp = torch.empty((h, w, 4), device=dev)
         st = torch.zeros((h, w), dtype=torch.int32, device=dev)
@@ -156,7 +157,7 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         assert int(cnt[1]) > 24 * int(cnt[0]) // 2   # >= 1 aniso level per step on average
     # bits 20-23: diffuse parts of the split (3, 4 -> 3 parts of 3 cones, 5, 9 -> one cone each)
     for variant in (0, 1, 0x100, 0x200, 0x400, 0x800, 0x400, 0x300400, 0x400400, 0x500400, 0x900400, 0x900400,
-                    0x500400, 0):
+                    0x500400, 0, 0x8000, 0x8400, 0x8800, 0x8200, 0x8000):
         d = torch.full((h, w, 4), -1.0, device=dev)
         sp = torch.full((h, w, 4), -1.0, device=dev)
         cnt = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -865,3 +866,43 @@ def test_gbuffer_projects_to_pixel_centres(gpu_ready, case, size):
     assert err.max() <= 1e-3, (err.max(), np.argmax(err))
     assert np.all((ndc[:, 2] > -1) & (ndc[:, 2] < 1))     # inside GLM's depth range (near 0.1, far 100)
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["rand", "scene"])
+def test_reorder_equals_screen_order(gpu_ready, kind):
+    """Ray reordering (variant 0x8000) at the metric size (256^3, 1080p, 9 + 1 cones):
+    the outputs, per-pixel step counts and step counter equal the screen-order trace
+    bit for bit, for the incoherent G_rand it is meant for and for G_scene; the timed
+    launch form (no counters) too."""
+    import torch
+    from vct import scenes
+    n, w, h = 256, 1920, 1080
+    ctx, s, arrs, (g0, E) = gpu_pipeline(n, "atrium")
+    from vct.camera import Camera
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    cam = Camera()
+    if kind == "scene":
+        gb = [torch.empty((h, w, 4), device=dev) for _ in range(3)]
+        ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)
+    else:
+        ao, nm = ctx.download_voxels()
+        gb = [torch.from_numpy(x).to(dev) for x in scenes.gbuffer_rand(ao, nm, g0, E, w, h, seed=42)]
+    outs = {}
+    for variant in (0, 0x8000):
+        d = torch.full((h, w, 4), -1.0, device=dev)
+        sp = torch.full((h, w, 4), -1.0, device=dev)
+        st = torch.zeros((h, w), dtype=torch.int32, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        ctx.trace_device(*gb, w, h, cam.position, d, sp, steps_px=st, cone_steps=cnt, variant=variant)
+        d2 = torch.full((h, w, 4), -1.0, device=dev)
+        sp2 = torch.full((h, w, 4), -1.0, device=dev)
+        ctx.trace_device(*gb, w, h, cam.position, d2, sp2, variant=variant)   # timed form
+        torch.cuda.synchronize()
+        outs[variant] = (d, sp, st, int(cnt[0]), d2, sp2)
+    a, b = outs[0], outs[0x8000]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), "reordered outputs differ"
+    assert torch.equal(a[2], b[2]) and a[3] == b[3], "reordered step counts differ"
+    assert torch.equal(b[4], a[0]) and torch.equal(b[5], a[1]), "reordered timed form differs"
+    assert torch.equal(a[4], a[0]) and torch.equal(a[5], a[1])

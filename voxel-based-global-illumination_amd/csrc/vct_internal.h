@@ -53,10 +53,10 @@ struct vct_ctx {
     hipStream_t stream = nullptr;
     vct::Grid grid;
     vct::Mesh mesh;
-    vct::Scratch scratch[10];     // reusable scratch (0 trace host staging, 1 voxelize temps,
+    vct::Scratch scratch[12];     // reusable scratch (0 trace host staging, 1 voxelize temps,
                                   // 2-3 G-buffer bins, 4 K2 work list, 5-6 K4 cone-split hand-over,
                                   // 7 K1 candidate bucket table, 8 multi-device tiles / gather,
-                                  // 9 multi-device step counters)
+                                  // 9 multi-device step counters, 10-11 ray reorder keys / sort temps)
     vct::StepRow* step_tab = nullptr;   // [kMaxStepRows] diffuse-cone step table (device)
     unsigned* spec_keys = nullptr;      // [2 * kSpecSlots]: specular table keys (~0u free), then states
     vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)
@@ -85,6 +85,9 @@ hipError_t launch_mips(vct_ctx* c);
 hipError_t launch_relayout(vct_ctx* c, const float4* src, float4* dst, uint32_t nl, bool to_linear);
 // K4
 hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a);
+// ray reordering (variant 0x8000, vct_reorder.hip): *perm = the frame's pixels sorted by the
+// Morton code of their cone origin's voxel, background last (device, w * h entries)
+hipError_t launch_reorder(vct_ctx* c, const vct_trace_args* a, const uint32_t** perm);
 hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t planes, uint32_t w, uint32_t h,
                          uint32_t world, float4* const* frames, bool packed = false);
 // composite + present (row f3)

@@ -151,6 +151,8 @@ struct TraceK {
     float4* sc_cone;             // split 2: [cone - nd_chunk][px] results of cones [nd_chunk, nd)
     size_t sc_px;                // pixels per scratch plane
     unsigned* sc_flag;           // split 2: [block][wave] hand-over counter (0 between launches)
+    const uint32_t* perm;        // ray reordering (variant 0x8000): lane j of wave u traces pixel perm[64 u + j]
+    uint32_t npx;                // its length (w * h)
 };
 
 __device__ __forceinline__ const float (*cone_table(int nd))[4] {
@@ -1109,7 +1111,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         }
         const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
         // a >= 0.95, t > tmax or outside the grid ends the lane's march (no short-circuit branches)
-        const bool inside = (fminf(fminf(qx, qy), qz) >= 0.0f) & (fmaxf(fmaxf(qx, qy), qz) <= nf);
+        const bool inside = (int)(fminf(fminf(qx, qy), qz) >= 0.0f) & (int)(fmaxf(fmaxf(qx, qy), qz) <= nf);
         active = active & (a < VCT_ALPHA_STOP) & (t <= k.tmax) & inside;
         const unsigned long long am = wballot(active);
         if (am == 0ull) break;
@@ -1243,12 +1245,20 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     const uint32_t my = MORTON ? ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4) : lane >> 3;
     const uint32_t px = (sub & 3) * 16 + (wave & 1) * 8 + mx;
     const uint32_t py = (sub >> 2) * 16 + (wave >> 1) * 8 + my;
-    const uint32_t tile = lt * (uint32_t)k.world + (uint32_t)k.rank;
-    const uint32_t x = (tile % (uint32_t)k.tiles_x) * VCT_TILE + px;
-    const uint32_t y = (tile / (uint32_t)k.tiles_x) * VCT_TILE + py;
-    const bool in_frame = x < (uint32_t)k.w && y < (uint32_t)k.h;
-    const size_t pix = in_frame ? (size_t)y * (size_t)k.w + x : 0;
-    const size_t oidx = k.compact ? (size_t)lt * (VCT_TILE * VCT_TILE) + py * VCT_TILE + px : pix;
+    bool in_frame;
+    size_t pix, oidx;
+    if (k.perm) {                                // reordered rays: whole frame, outputs at the pixel
+        const uint32_t si = (rb * 4u + wave) * 64u + lane;
+        in_frame = si < k.npx;
+        pix = oidx = in_frame ? k.perm[si] : 0u;
+    } else {
+        const uint32_t tile = lt * (uint32_t)k.world + (uint32_t)k.rank;
+        const uint32_t x = (tile % (uint32_t)k.tiles_x) * VCT_TILE + px;
+        const uint32_t y = (tile / (uint32_t)k.tiles_x) * VCT_TILE + py;
+        in_frame = x < (uint32_t)k.w && y < (uint32_t)k.h;
+        pix = in_frame ? (size_t)y * (size_t)k.w + x : 0;
+        oidx = k.compact ? (size_t)lt * (VCT_TILE * VCT_TILE) + py * VCT_TILE + px : pix;
+    }
 
     float4 dout = make_float4(0.0f, 0.0f, 0.0f, 0.0f), sout = dout;
     uint32_t steps = 0, texels = 0;
@@ -1448,8 +1458,17 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         k.xcd_g = g_of[m < 7 ? m : 0];
     }
     k.sc_part = k.sc_cone = nullptr; k.sc_flag = nullptr; k.sc_px = 0;
-    const uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
+    k.perm = nullptr;
+    k.npx = a->width * a->height;
+    uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
+    if ((a->variant & 0x8000) && world == 1 && !k.compact) {
+        // ray reordering (full frame, one rank): waves take 64 consecutive entries of the
+        // sorted pixel list; nlt counts 64-wave units of it instead of 64x64 tiles
+        hipError_t e = launch_reorder(c, a, &k.perm);
+        if (e != hipSuccess) return e;
+        nlt = (k.npx + 64u * 64u - 1u) / (64u * 64u);
+    }
     const bool wg1 = !(a->variant & 0x1000);    // 0x1000: four waves per workgroup
     uint32_t blocks = nlt * 16;
     if (k.split && k.nd > 1 && ((a->variant & 0x400) || (!(a->variant & 0x800) && blocks <= kSplit3MaxBlocks))) {
