@@ -89,6 +89,9 @@ def parse():
                    help="N > 1: assemble the frame on rank 0 (send/recv) or on every rank (all-gather)")
     p.add_argument("--secondary", default="courtyard",
                    help="second scene measured at the same size (empty or 'none': skip)")
+    p.add_argument("--stress", default="rand",
+                   help="N = 1: also time the cache-hostile G_rand G-buffer on the metric scene, screen "
+                        "order vs ray reordering (empty or 'none': skip)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-json", default=PROFILE)
@@ -479,6 +482,47 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     return r
 
 
+def stress_rand(args, torch, ctx, dev, stream):
+    """G_rand (independent random surface points and normals per pixel) on the
+    scene in `ctx`: the K4 pass in screen order and with ray reordering (variant 0x8000),
+    timed alike; both must be bit-identical."""
+    from vct import scenes
+    from vct.camera import Camera
+    w, h = args.width, args.height
+    ao, nm = ctx.download_voxels()
+    gb = tuple(torch.from_numpy(a).to(dev) for a in scenes.gbuffer_rand(ao, nm, ctx.aabb_min, ctx.extent, w, h,
+                                                                         seed=42))
+    del ao, nm
+    eye = [float(x) for x in Camera().position]
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    outs, ms = {}, {}
+    reps = max(3, args.steps // 4)
+    for v in (args.variant & ~0x8000, args.variant | 0x8000):
+        d = torch.empty((h, w, 4), device=dev)
+        sp = torch.empty((h, w, 4), device=dev)
+        if v & 0x8000 == 0:
+            ctx.trace_device(*gb, w, h, eye, d, sp, cone_steps=cnt, variant=v)
+        ctx.trace_device(*gb, w, h, eye, d, sp, variant=v)     # warm
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        torch.cuda.synchronize()
+        e[0].record(stream)
+        for _ in range(reps):
+            ctx.trace_device(*gb, w, h, eye, d, sp, variant=v)
+        e[1].record(stream)
+        torch.cuda.synchronize()
+        ms[v] = e[0].elapsed_time(e[1]) / reps
+        outs[v] = (d, sp)
+    steps = int(cnt[0].item())
+    (a0, a1), (b0, b1) = outs.values()
+    t0, t1 = ms.values()
+    return {"gbuffer": "G_rand (seed 42), same grid", "frame_cone_steps": steps, "frames": reps,
+            "screen_order_ms": round(t0, 4), "reordered_ms": round(t1, 4),
+            "screen_order_Mcone_steps_s": round(steps / t0 / 1e3, 2),
+            "reordered_Mcone_steps_s": round(steps / t1 / 1e3, 2),
+            "speedup": round(t0 / t1, 3),
+            "bitexact": bool(torch.equal(a0, b0) and torch.equal(a1, b1))}
+
+
 def run(args, world):
     import numpy as np
     import torch
@@ -553,6 +597,10 @@ def run(args, world):
                                                   m["_steps_px"].cpu().numpy().astype(np.uint32), args.cpu_seconds)
     del m
     torch.cuda.empty_cache()
+    st = (args.stress or "").strip()
+    if st == "rand" and world == 1 and args.gbuffer == "scene":
+        result["stress"] = stress_rand(args, torch, ctx, dev, stream)
+        torch.cuda.empty_cache()
     sec = (args.secondary or "").strip()
     if sec and sec != "none" and sec != args.scene:
         # the same size on a non-flat scene (varied normals: fewer combined-face bricks)
