@@ -164,6 +164,13 @@ vct_status vct_trace(vct_ctx* ctx, const float* gbuf_pos4, const float* gbuf_nrm
                      uint32_t* out_steps_px, uint64_t* out_cone_steps);
 /* Device-resident form (asynchronous on the ctx stream). */
 vct_status vct_trace_device(vct_ctx* ctx, const vct_trace_args* args);
+/* The default variant has two bit-identical compiled forms: 0 the four-face-union form
+ * (4 waves/SIMD), 1 the occupancy form (5 waves/SIMD, three-face bricks).  The context
+ * times both on its first counter-free launches of a workload (frame size, tiling, scene,
+ * cone set; HIP events read back without blocking) and keeps the faster one.  Returns the
+ * form of the current workload, or -1 while it is still being timed.  Variant bits
+ * 0x1000000 / 0x2000000 force form 0 / 1. */
+int32_t    vct_trace_form(const vct_ctx* ctx);
 /* Number of 64x64 tiles rank `rank` of `world` traces for a width x height frame. */
 uint32_t   vct_tiles_for_rank(uint32_t width, uint32_t height, uint32_t rank, uint32_t world);
 /* Scatter all-gathered rank-compact tile buffers ([world][max_tiles][64*64][4],

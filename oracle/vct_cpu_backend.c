@@ -120,6 +120,8 @@ vct_status vct_create_multi(const vct_config* cfg, uint32_t n_devices, vct_ctx**
 }
 
 uint32_t vct_num_devices(const vct_ctx* c) { return c ? (c->ndev ? c->ndev : 1u) : 0u; }
+/* one CPU code path: no forms to choose between */
+int32_t vct_trace_form(const vct_ctx* c) { (void)c; return 0; }
 
 vct_status vct_set_stream(vct_ctx* c, void* s) { (void)s; return c ? VCT_OK : VCT_EINVAL; }
 vct_status vct_synchronize(vct_ctx* c) { return c ? VCT_OK : VCT_EINVAL; }

@@ -142,7 +142,8 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
     gb = [torch.from_numpy(a).to(dev) for a in (pos, nrm, alb)]
     ref = O.trace(n, g0, E, ctx.download_level(0), gpu_pyramid_flat(ctx), pos, nrm, alb, cam.position)
     # 0x8000: rays reordered by the Morton code of their origin voxel (alone, with gathers, without the union)
-    for variant in (0, 1, 2, 3, 0x8000, 0x8001, 0x8002):
+    # 0x1000000 / 0x2000000: the union / occupancy form of the default variant
+    for variant in (0, 1, 2, 3, 0x8000, 0x8001, 0x8002, 0x1000000, 0x2000000, 0x2008000):
         d = torch.empty((h, w, 4), device=dev)
         sp = torch.empty((h, w, 4), device=dev)
         st = torch.zeros((h, w), dtype=torch.int32, device=dev)
@@ -157,7 +158,8 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         assert int(cnt[1]) > 24 * int(cnt[0]) // 2   # >= 1 aniso level per step on average
     # bits 20-23: diffuse parts of the split (3, 4 -> 3 parts of 3 cones, 5, 9 -> one cone each)
     for variant in (0, 1, 0x100, 0x200, 0x400, 0x800, 0x400, 0x300400, 0x400400, 0x500400, 0x900400, 0x900400,
-                    0x500400, 0, 0x8000, 0x8400, 0x8800, 0x8200, 0x8000):
+                    0x500400, 0, 0x8000, 0x8400, 0x8800, 0x8200, 0x8000, 0x1000000, 0x2000000, 0x2000400,
+                    0x2000800, 0x2001000, 0x2008000):
         d = torch.full((h, w, 4), -1.0, device=dev)
         sp = torch.full((h, w, 4), -1.0, device=dev)
         cnt = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -906,3 +908,38 @@ def test_reorder_equals_screen_order(gpu_ready, kind):
     assert torch.equal(a[2], b[2]) and a[3] == b[3], "reordered step counts differ"
     assert torch.equal(b[4], a[0]) and torch.equal(b[5], a[1]), "reordered timed form differs"
     assert torch.equal(a[4], a[0]) and torch.equal(a[5], a[1])
+
+
+@pytest.mark.gpu
+def test_trace_form_tuner(gpu_ready):
+    """The default variant times its two compiled forms on the first counter-free launches
+    of a workload and keeps the faster one (vct_trace_form): every launch, whichever form
+    ran it, gives the same bits as the counting form; the choice is made within a few
+    dozen frames and restarts for a new workload (frame size)."""
+    import torch
+    from vct import scenes
+    from vct.camera import Camera
+    n = 128
+    ctx, s, arrs, (g0, E) = gpu_pipeline(n, "atrium")
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    cam = Camera()
+    for w, h in ((320, 200), (256, 128)):
+        gb = [torch.empty((h, w, 4), device=dev) for _ in range(3)]
+        ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)
+        ref_d = torch.empty((h, w, 4), device=dev)
+        ref_s = torch.empty((h, w, 4), device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        ctx.trace_device(*gb, w, h, cam.position, ref_d, ref_s, cone_steps=cnt)   # counting form
+        assert ctx.trace_form == -1 or w != 320
+        d = torch.empty_like(ref_d)
+        sp = torch.empty_like(ref_s)
+        for i in range(64):
+            d.fill_(-1.0)
+            sp.fill_(-1.0)
+            ctx.trace_device(*gb, w, h, cam.position, d, sp)
+            torch.cuda.synchronize()
+            assert torch.equal(d, ref_d) and torch.equal(sp, ref_s), f"launch {i} (form {ctx.trace_form})"
+            if ctx.trace_form >= 0:
+                break
+        assert ctx.trace_form in (0, 1), "no form chosen after 64 launches"

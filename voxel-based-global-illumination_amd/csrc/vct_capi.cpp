@@ -205,6 +205,7 @@ vct_status vct_create_multi(const vct_config* cfg, uint32_t n_devices, vct_ctx**
 }
 
 uint32_t vct_num_devices(const vct_ctx* c) { return c ? 1u + (uint32_t)c->peers.size() : 0u; }
+int32_t vct_trace_form(const vct_ctx* c) { return c ? c->k4tune.chosen : -1; }
 
 void vct_destroy(vct_ctx* c) {
     if (!c) return;
@@ -230,6 +231,10 @@ void vct_destroy(vct_ctx* c) {
     for (auto& s : c->scratch)
         if (s.p) (void)hipFree(s.p);
     if (c->ev) (void)hipEventDestroy(c->ev);
+    for (auto& f : c->k4tune.ev)
+        for (auto& sl : f)
+            for (hipEvent_t e : sl)
+                if (e) (void)hipEventDestroy(e);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -290,6 +295,7 @@ static vct_status voxelize_dev(vct_ctx* c, const void* dv, uint32_t stride, uint
     // a grid from out-of-range indices is partial: inject / mips / trace refuse it (VCT_ESTATE)
     c->grid.voxelized = herr == 0;
     c->grid.injected = c->grid.mipped = false;
+    ++c->grid_epoch;
     if (herr) return fail(c, VCT_EINVAL, "vertex or material index out of range");
     return VCT_OK;
 }
@@ -457,7 +463,8 @@ vct_status vct_trace_device(vct_ctx* c, const vct_trace_args* a) {
     if (!c->grid.mipped) return fail(c, VCT_ESTATE, "trace before build_mips");
     if (!a->pos4 || !a->nrm4 || !a->alb4 || !a->diffuse4 || !a->spec4)
         return fail(c, VCT_EINVAL, "null G-buffer or output pointer");
-    if (a->width == 0 || a->height == 0 || a->width > 65536 || a->height > 65536)
+    if (a->width == 0 || a->height == 0 || a->width > 65536 || a->height > 65536 ||
+        (uint64_t)a->width * a->height > 0xffffffffull)   // K4 indexes pixels with 32 bits
         return fail(c, VCT_EINVAL, "bad frame size");
     if (a->tile_world > 1 && a->tile_rank >= a->tile_world) return fail(c, VCT_EINVAL, "tile_rank >= tile_world");
     // the counters are 64-bit device atomics: a misaligned target faults the GPU

@@ -125,7 +125,8 @@ vct_status vct_comm_trace_frame(vct_ctx* c, const vct_trace_args* a, int32_t roo
     if (root != VCT_ALL_RANKS && (root < 0 || root >= c->comm_size))
         return cfail(c, VCT_EINVAL, "trace_frame: root out of range");
     if (a->tile_world > 1 || a->tile_compact) return cfail(c, VCT_EINVAL, "trace_frame sets the tiling itself");
-    if (a->width == 0 || a->height == 0 || a->width > 65536 || a->height > 65536)
+    if (a->width == 0 || a->height == 0 || a->width > 65536 || a->height > 65536 ||
+        (uint64_t)a->width * a->height > 0xffffffffull)   // K4 indexes pixels with 32 bits
         return cfail(c, VCT_EINVAL, "bad frame size");
     const uint32_t R = (uint32_t)c->comm_size, me = (uint32_t)c->comm_rank;
     const bool all = root == VCT_ALL_RANKS;

@@ -45,6 +45,30 @@ struct Scratch {
     size_t bytes = 0;
 };
 
+// K4 form choice (vct_trace.hip k4_form).  The default cone trace has two bit-identical
+// compiled forms: the four-face-union form (4 waves/SIMD; pays on curved surfaces, where
+// a wave's lanes straddle an axis) and the occupancy form (5 waves/SIMD, three-face
+// bricks; pays on flat ones).  A context times both on its first timed launches of a
+// workload (HIP events on its stream; while timing, a launch first waits for the previous
+// timed one to finish, so the choice is made within 7 launches even when the host queues
+// frames far ahead), keeps the faster one, and re-times after kRetune launches or when
+// the workload changes.
+struct K4Tuner {
+    static constexpr int kSlots = 4;          // event pairs in flight per form
+    static constexpr int kSamples = 2;        // timed samples per form after the first (cold) one
+    static constexpr uint32_t kRetune = 4096;
+    uint64_t key = ~0ull;                     // workload the state belongs to
+    int chosen = -1;                          // 0 union form, 1 occupancy form; -1 still timing
+    uint32_t since = 0;                       // timed launches since the choice
+    uint32_t launches = 0;                    // timed launches while choosing
+    hipEvent_t ev[2][kSlots][2] = {};
+    bool busy[2][kSlots] = {};
+    int head[2] = {0, 0};
+    int seen[2] = {0, 0};                     // completed samples (the first one is dropped)
+    float best[2] = {0.0f, 0.0f};             // fastest completed sample, ms
+    hipEvent_t last = nullptr;                // end event of the previous timed launch while timing
+};
+
 }  // namespace vct
 
 struct vct_ctx {
@@ -57,6 +81,8 @@ struct vct_ctx {
                                   // 2-3 G-buffer bins, 4 K2 work list, 5-6 K4 cone-split hand-over,
                                   // 7 K1 candidate bucket table, 8 multi-device tiles / gather,
                                   // 9 multi-device step counters, 10-11 ray reorder keys / sort temps)
+    vct::K4Tuner k4tune;                // timed-form choice of the default cone trace
+    uint32_t grid_epoch = 0;            // bumped by every voxelization (a new scene for the tuner)
     vct::StepRow* step_tab = nullptr;   // [kMaxStepRows] diffuse-cone step table (device)
     unsigned* spec_keys = nullptr;      // [2 * kSpecSlots]: specular table keys (~0u free), then states
     vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)

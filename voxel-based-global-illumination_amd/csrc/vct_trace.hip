@@ -104,6 +104,12 @@ __device__ __forceinline__ float lvl_coord(float q, float scale) {
     return fmaf(q, scale, -0.5f);
 }
 
+#ifndef VCT_K4_SLIM
+#define VCT_K4_SLIM 1     // fewer registers held over the march (frame rebuilt per cone, P / n re-read)
+#endif
+// the occupancy form of the default cone trace: 96 VGPRs, 7008 B of LDS (no four-face
+// union), 5 waves/SIMD; the union form keeps VCT_K4_MIN_WAVES (K4Tuner picks per workload)
+constexpr int kOccWaves = 5;
 #ifndef VCT_K4_MIN_WAVES
 #define VCT_K4_MIN_WAVES 4      // __launch_bounds__ minimum waves per SIMD of K4 (128 VGPRs)
 #endif
@@ -191,6 +197,9 @@ __device__ __forceinline__ float4 combine3(float wx, float wy, float wz, float4 
 #define VCT_KCH 4
 #endif
 constexpr int kCh = VCT_KCH;
+// the occupancy form (5 waves/SIMD, 96 VGPRs) keeps 2 corners x 3 faces in flight
+constexpr int kChOcc = 2;
+template <bool UNION> constexpr int gather_chunk() { return UNION ? kCh : kChOcc; }
 
 // trilinear corner weights (x fastest), w_c = (wx * wy) * wz
 __device__ __forceinline__ void corner_weights(float fx, float fy, float fz, float (&wc)[8]) {
@@ -286,6 +295,7 @@ __device__ __forceinline__ LevelBits level_bits(const TraceK& k, int l) {
 
 // D_l for a wave-uniform level through its buffer resource (O32, brick layout):
 // same texels, weights and fmaf order as sample_level
+template <int KC>
 __device__ __forceinline__ float4 sample_level_bits(const TraceK& k, int l, float qx, float qy, float qz, int fx,
                                                     int fy, int fz, float wdx, float wdy, float wdz) {
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
@@ -323,16 +333,16 @@ __device__ __forceinline__ float4 sample_level_bits(const TraceK& k, int l, floa
     }
     const uint32_t FX = (uint32_t)fx << lb.shf, FY = (uint32_t)fy << lb.shf, FZ = (uint32_t)fz << lb.shf;
 #pragma unroll
-    for (int h = 0; h < 8; h += kCh) {         // kCh corners x 3 faces in flight
-        float4 vx[kCh], vy[kCh], vz[kCh];
+    for (int h = 0; h < 8; h += KC) {          // KC corners x 3 faces in flight
+        float4 vx[KC], vy[KC], vz[KC];
 #pragma unroll
-        for (int c = 0; c < kCh; ++c) {
+        for (int c = 0; c < KC; ++c) {
             vx[c] = ld(off[h + c] | FX);
             vy[c] = ld(off[h + c] | FY);
             vz[c] = ld(off[h + c] | FZ);
         }
 #pragma unroll
-        for (int c = 0; c < kCh; ++c) acc_fma(acc, wc[h + c], combine3(wdx, wdy, wdz, vx[c], vy[c], vz[c]));
+        for (int c = 0; c < KC; ++c) acc_fma(acc, wc[h + c], combine3(wdx, wdy, wdz, vx[c], vy[c], vz[c]));
         __builtin_amdgcn_sched_barrier(0);     // keep the next chunk's loads below (VGPR budget)
     }
     return acc;
@@ -341,11 +351,11 @@ __device__ __forceinline__ float4 sample_level_bits(const TraceK& k, int l, floa
 // D_l(q, d) (A.5): level 0 / isotropic = T_l; anisotropic = faces combined per
 // corner texel, then trilinear.  Zero border: out-of-range corners read as 0
 // (LevelView); fmaf(w, 0, acc) == acc, the spec's zero-border sum.
-template <bool O32, bool UNIF = false>   // UNIF: l is wave-uniform (buffer resource); else per lane
+template <bool O32, bool UNIF = false, int KC = kCh>   // UNIF: l wave-uniform (buffer resource); else per lane
 __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx, float qy, float qz,
                                                int fx, int fy, int fz, float wdx, float wdy, float wdz) {
 #if VCT_BRICK2
-    if constexpr (O32 && UNIF) return sample_level_bits(k, l, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+    if constexpr (O32 && UNIF) return sample_level_bits<KC>(k, l, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
 #endif
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
     const int nl = k.n >> l;
@@ -415,16 +425,16 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
     const uint32_t vl = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
     const uint32_t X = (uint32_t)fx * vl, Y = (uint32_t)fy * vl, Z = (uint32_t)fz * vl;
 #pragma unroll
-    for (int h = 0; h < 8; h += kCh) {         // kCh corners x 3 faces in flight
-        float4 vx[kCh], vy[kCh], vz[kCh];
+    for (int h = 0; h < 8; h += KC) {          // KC corners x 3 faces in flight
+        float4 vx[KC], vy[KC], vz[KC];
 #pragma unroll
-        for (int c = 0; c < kCh; ++c) {
+        for (int c = 0; c < KC; ++c) {
             vx[c] = lv.fetch(X + idx[h + c], in[h + c]);
             vy[c] = lv.fetch(Y + idx[h + c], in[h + c]);
             vz[c] = lv.fetch(Z + idx[h + c], in[h + c]);
         }
 #pragma unroll
-        for (int c = 0; c < kCh; ++c) acc_fma(acc, wc[h + c], combine3(wdx, wdy, wdz, vx[c], vy[c], vz[c]));
+        for (int c = 0; c < KC; ++c) acc_fma(acc, wc[h + c], combine3(wdx, wdy, wdz, vx[c], vy[c], vz[c]));
         __builtin_amdgcn_sched_barrier(0);     // keep the next chunk's loads below (VGPR budget)
     }
     return acc;
@@ -501,7 +511,10 @@ __device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, f
 constexpr int kBz = 19;
 constexpr int kBlk = 3 * kBz + 16;              // one face block: 73 slots
 // float4 slots per cache entry: up to 4 face blocks (3 without the four-face union)
+// The two cache entries live in LDS regions 0 and 1 (entry a in region `flip`): 9344 B
+// per wave with the union (4 waves/SIMD fit the 160 KB), 7008 B without (5 waves/SIMD).
 template <bool UNION> constexpr int entry_slots() { return (UNION ? 4 : 3) * kBlk; }
+template <bool UNION> constexpr int lds_slots() { return 2 * entry_slots<UNION>(); }
 
 // One wave's LDS hand-off (writes -> other lanes' reads, and reads -> next
 // writes): the asm "memory" clobber keeps the compiler from moving DS ops
@@ -645,6 +658,14 @@ __device__ __forceinline__ bool in_quad(int cx, int cy, int cz, uint32_t qo) {
 
 enum { kIso = 0, kComb = 1, kFaces = 2 };
 
+// the lane id, re-derived where it is used: the staging offsets built from it would
+// otherwise be hoisted out of the march and held in VGPRs for its whole length
+__device__ __forceinline__ int lane_id_opaque() {
+    int lane = (int)threadIdx.x;
+    asm volatile("" : "+v"(lane));
+    return lane & 63;
+}
+
 struct Tex4 { float4 a, b, c, d; };
 
 // this lane's staging texel: iso -> a; comb / faces -> faces f0..f3 of the union in a..d
@@ -652,7 +673,7 @@ template <bool O32>
 __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEntry& be, int mode,
                                            const ConeCtl& cc) {
     const int nl = k.n >> l;
-    const int lane = threadIdx.x & 63;
+    const int lane = lane_id_opaque();
     const int sx = be.ox + (lane & 3), sy = be.oy + ((lane >> 2) & 3), sz = be.oz + (lane >> 4);
     const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
     const uint32_t gi = texel_index_lg((uint32_t)sx, (uint32_t)sy, (uint32_t)sz, (uint32_t)(k.lgn - l));
@@ -686,7 +707,7 @@ __device__ __forceinline__ uint32_t bits4(float4 v) {
 
 // stores this lane's staging texel(s); returns true when every value it stored is +0
 __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const Tex4& t, float4* __restrict__ lds) {
-    const int lane = threadIdx.x & 63;
+    const int lane = lane_id_opaque();
     float4* p = lds + ((lane & 15) + kBz * (lane >> 4));
     uint32_t nz;
     if (mode == kIso) {
@@ -805,13 +826,31 @@ __device__ __forceinline__ void dbg_fallback_reason(const Corner& c, bool active
 #endif
 }
 
+// A lane's cone direction as the step code reads it: the faces it selects (signs of
+// d), their weights d^2 and its face blocks in a faces-mode brick.  Derived on use from
+// d and a 6-bit block code rather than held in 9 VGPRs over the march: march_brick
+// passes d and the code through an empty asm at every step, so LLVM cannot hoist the
+// derivations back out of the loop (a few VALU in the faces-mode / gather paths only).
+struct LaneDir {
+    float dx, dy, dz;
+    uint32_t blk;                // bits 0-1 / 2-3 / 4-5: the x / y / z face's block index in the union
+    __device__ int fx() const { return dx >= 0.0f ? VCT_FACE_PX : VCT_FACE_NX; }
+    __device__ int fy() const { return dy >= 0.0f ? VCT_FACE_PY : VCT_FACE_NY; }
+    __device__ int fz() const { return dz >= 0.0f ? VCT_FACE_PZ : VCT_FACE_NZ; }
+    __device__ float wx() const { return dx * dx; }
+    __device__ float wy() const { return dy * dy; }
+    __device__ float wz() const { return dz * dz; }
+    __device__ int bx() const { return __mul24(kBlk, (int)(blk & 3u)); }
+    __device__ int by() const { return __mul24(kBlk, (int)((blk >> 2) & 3u)); }
+    __device__ int bz() const { return __mul24(kBlk, (int)(blk >> 4)); }
+};
+
 // One step's blended sample (1 - fr) D_{l0} + fr D_{l0+1} for a wave-uniform l0.
 // Each level is served from the cache, restaged (both levels' loads in one
 // batch) or, when the wave's footprint does not fit, gathered per lane.
 template <bool O32, bool UNION, int KL>
 __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx, float qy, float qz, bool active,
-                                              bool two, float fr, const ConeCtl& cc, int fx, int fy, int fz, int bx,
-                                              int by, int bz, float wdx, float wdy, float wdz,
+                                              bool two, float fr, const ConeCtl& cc, const LaneDir& ld,
                                               float4* __restrict__ lds, BrickCache& bc, PhaseClock& pc) {
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const bool activeB = active && two;
@@ -835,6 +874,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     }
     float4* ldsA = lds + bc.flip * entry_slots<UNION>();
     float4* ldsB = lds + (bc.flip ^ 1) * entry_slots<UNION>();
+    const bool faces_okA = faces_ok, faces_okB = faces_ok;
     // level A: cached, restaged, or gathered
     const Corner cA = level_corner(l0, qx, qy, qz);
     BrickEntry bA = bc.a;
@@ -843,7 +883,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     };
     bool useA = bA.lvl == l0 && wall_in(amA, fits(cA, bA, bc.qa));
     bool stA = false;
-    if (!useA && (modeA != kFaces || faces_ok)) {
+    if (!useA && (modeA != kFaces || faces_okA)) {
         BrickEntry nb{};
         nb.lvl = l0;
         if (brick_origin(cA, amA, cc.neg, nb)) {
@@ -867,7 +907,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     if (needB) {
         cB = level_corner(l1, qx, qy, qz);
         useB = bB.lvl == l1 && wall_in(amB, fits(cB, bB, bc.qb));
-        if (!useB && (modeB != kFaces || faces_ok)) {
+        if (!useB && (modeB != kFaces || faces_okB)) {
             BrickEntry nb{};
             nb.lvl = l1;
             if (brick_origin(cB, amB, cc.neg, nb)) {
@@ -931,21 +971,23 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     if (useA) VCT_DBG(bA.zero ? 17 : 15);          // level-A samples from zero / nonzero bricks
     if (readA || readB) {
         if (readA && active)
-            sA = brick_sample<KL>(cA, brick_slot(cA, bA, bc.qa), modeA != kFaces, bx, by, bz, wdx, wdy, wdz, ldsA);
+            sA = brick_sample<KL>(cA, brick_slot(cA, bA, bc.qa), modeA != kFaces, ld.bx(), ld.by(), ld.bz(), ld.wx(),
+                                  ld.wy(), ld.wz(), ldsA);
         if (readB && activeB)
-            sB = brick_sample<KL>(cB, brick_slot(cB, bB, bc.qb), modeB != kFaces, bx, by, bz, wdx, wdy, wdz, ldsB);
+            sB = brick_sample<KL>(cB, brick_slot(cB, bB, bc.qb), modeB != kFaces, ld.bx(), ld.by(), ld.bz(), ld.wx(),
+                                  ld.wy(), ld.wz(), ldsB);
         wave_lds_sync();
     }
     pc.mark(3);
     if (!useA) {
         VCT_DBG(4 + (l0 < 10 ? l0 : 10));
-        dbg_fallback_reason(cA, active, modeA != kFaces || faces_ok, l0);
-        if (active) sA = sample_level<O32, true>(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+        dbg_fallback_reason(cA, active, modeA != kFaces || faces_okA, l0);
+        if (active) sA = sample_level<O32, true, gather_chunk<UNION>()>(k, l0, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(), ld.wy(), ld.wz());
     }
     if (needB && !useB) {
         VCT_DBG(4 + (l1 < 10 ? l1 : 10));
-        dbg_fallback_reason(cB, activeB, modeB != kFaces || faces_ok, l1);
-        if (activeB) sB = sample_level<O32, true>(k, l1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
+        dbg_fallback_reason(cB, activeB, modeB != kFaces || faces_okB, l1);
+        if (activeB) sB = sample_level<O32, true, gather_chunk<UNION>()>(k, l1, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(), ld.wy(), ld.wz());
     }
     pc.mark(4);
     return activeB ? blend(sA, sB, fr) : sA;
@@ -1070,7 +1112,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     uint32_t steps = 0;
     bool active = valid;
     ConeCtl cc;
-    int bx, by, bz;              // this lane's face blocks in a faces-mode brick (float4 offsets)
+    LaneDir ld;
     {
         const unsigned long long vm = wballot(valid);
         const int fl = vm ? __builtin_ctzll(vm) : 0;
@@ -1087,9 +1129,9 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.f2 = __builtin_ctz(u | 64);
         u &= u - 1;
         cc.f3 = __builtin_ctz(u | 64);
-        bx = kBlk * __builtin_popcount(cc.funion & ((1 << fx) - 1));
-        by = kBlk * __builtin_popcount(cc.funion & ((1 << fy) - 1));
-        bz = kBlk * __builtin_popcount(cc.funion & ((1 << fz) - 1));
+        ld.blk = (uint32_t)__builtin_popcount(cc.funion & ((1 << fx) - 1)) |
+                 (uint32_t)__builtin_popcount(cc.funion & ((1 << fy) - 1)) << 2 |
+                 (uint32_t)__builtin_popcount(cc.funion & ((1 << fz) - 1)) << 4;
         cc.uwx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdx), fl));
         cc.uwy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdy), fl));
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
@@ -1101,6 +1143,8 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     bc.flip = 0;
     bc.qa = bc.qb = 0u;
     for (int i = 0;; ++i) {
+        asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz), "+v"(ld.blk));   // see LaneDir
+        ld.dx = dx; ld.dy = dy; ld.dz = dz;
         float D, fr;
         int l0;
         if constexpr (TAB) {                    // wave-uniform row i
@@ -1132,11 +1176,13 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         if (TAB || wall_in(am, l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
             __builtin_amdgcn_s_setprio(0);       // default priority for the step head, brick geometry and staging
-            s = step_bricks<O32, UNION, KL>(k, l0f, qx, qy, qz, active, two, fr, cc, fx, fy, fz, bx, by, bz, wdx, wdy,
-                                        wdz, lds, bc, pc);
+            s = step_bricks<O32, UNION, KL>(k, l0f, qx, qy, qz, active, two, fr, cc, ld, lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
-            s = sample_level<O32>(k, l0, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
-            if (two) s = blend(s, sample_level<O32>(k, l0 + 1, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz), fr);
+            s = sample_level<O32, false, gather_chunk<UNION>()>(k, l0, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(),
+                                                                  ld.wy(), ld.wz());
+            if (two)
+                s = blend(s, sample_level<O32, false, gather_chunk<UNION>()>(k, l0 + 1, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(), ld.wy(), ld.wz()),
+                          fr);
         }
         if (active) {
             if constexpr (CNT) {
@@ -1186,7 +1232,7 @@ __device__ __forceinline__ float4 ld_coherent(float4* p) {
 template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true, bool S3 = false,
           bool WG1 = true, bool CNT = true>
 __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
-    __shared__ float4 lds_all[BRICK && !WG1 ? 4 : 1][BRICK ? 2 * entry_slots<UNION>() : 1];
+    __shared__ float4 lds_all[BRICK && !WG1 ? 4 : 1][BRICK ? lds_slots<UNION>() : 1];
     // split: the grid is 2 or 3 parts over the same pixels, dispatched in
     // blockIdx order: split 1 = diffuse cones | specular cone; split 2 = diffuse
     // cones [0, c) | [c, 2c) | ... | specular (ndp diffuse parts of c = nd_chunk cones;
@@ -1246,7 +1292,7 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     const uint32_t px = (sub & 3) * 16 + (wave & 1) * 8 + mx;
     const uint32_t py = (sub >> 2) * 16 + (wave >> 1) * 8 + my;
     bool in_frame;
-    size_t pix, oidx;
+    uint32_t pix, oidx;                          // w * h < 2^32 (vct_trace_device)
     if (k.perm) {                                // reordered rays: whole frame, outputs at the pixel
         const uint32_t si = (rb * 4u + wave) * 64u + lane;
         in_frame = si < k.npx;
@@ -1256,8 +1302,8 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
         const uint32_t x = (tile % (uint32_t)k.tiles_x) * VCT_TILE + px;
         const uint32_t y = (tile / (uint32_t)k.tiles_x) * VCT_TILE + py;
         in_frame = x < (uint32_t)k.w && y < (uint32_t)k.h;
-        pix = in_frame ? (size_t)y * (size_t)k.w + x : 0;
-        oidx = k.compact ? (size_t)lt * (VCT_TILE * VCT_TILE) + py * VCT_TILE + px : pix;
+        pix = in_frame ? y * (uint32_t)k.w + x : 0u;
+        oidx = k.compact ? lt * (VCT_TILE * VCT_TILE) + py * VCT_TILE + px : pix;
     }
 
     float4 dout = make_float4(0.0f, 0.0f, 0.0f, 0.0f), sout = dout;
@@ -1277,18 +1323,23 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     if (run) {
         float4 N4 = make_float4(0.0f, 1.0f, 0.0f, 0.0f);
         if (valid) N4 = k.nrm[pix];
-        const float nx = N4.x, ny = N4.y, nz = N4.z;
+        float nx = N4.x, ny = N4.y, nz = N4.z;
         const float ox = (P.x - k.g0x) * k.inv_h + nx;
         const float oy = (P.y - k.g0y) * k.inv_h + ny;
         const float oz = (P.z - k.g0z) * k.inv_h + nz;
-        // Duff et al. 2017 branchless orthonormal basis
-        const float sgn = copysignf(1.0f, nz);
-        const float ka = -1.0f / (sgn + nz);
-        const float kb = (nx * ny) * ka;
-        const float Tx = 1.0f + ((sgn * nx) * nx) * ka, Ty = sgn * kb, Tz = -(sgn * nx);
-        const float Bx = kb, By = sgn + (ny * ny) * ka, Bz = -ny;
         const float(*cones)[4] = cone_table(k.nd);
         for (int c = S3 ? c_lo : 0; c < c_hi; ++c) {
+#if VCT_K4_SLIM
+            // the tangent frame is rebuilt per cone (a few VALU per ~12 steps) instead of
+            // holding 6 VGPRs over the march; the empty asm keeps LLVM from hoisting it
+            asm volatile("" : "+v"(nx), "+v"(ny), "+v"(nz));
+#endif
+            // Duff et al. 2017 branchless orthonormal basis
+            const float sgn = copysignf(1.0f, nz);
+            const float ka = -1.0f / (sgn + nz);
+            const float kb = (nx * ny) * ka;
+            const float Tx = 1.0f + ((sgn * nx) * nx) * ka, Ty = sgn * kb, Tz = -(sgn * nx);
+            const float Bx = kb, By = sgn + (ny * ny) * ka, Bz = -ny;
             const float cn = cones[c][0], ct = cones[c][1], cb = cones[c][2], wk = cones[c][3];
             const float dx = (cn * nx + ct * Tx) + cb * Bx;
             const float dy = (cn * ny + ct * Ty) + cb * By;
@@ -1310,6 +1361,14 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
         if (do_spec) {
 #else
         if (false) {
+#endif
+#if VCT_K4_SLIM
+            // position and normal are read again rather than held over the diffuse march
+            // (the compiler fence keeps the loads from being merged with the first ones)
+            asm volatile("" ::: "memory");
+            if (in_frame) P = k.pos[pix];
+            if (valid) N4 = k.nrm[pix];
+            nx = N4.x; ny = N4.y; nz = N4.z;
 #endif
             float vx = k.ex - P.x, vy = k.ey - P.y, vz = k.ez - P.z;
             float vl = sqrtf(dot3(vx, vy, vz, vx, vy, vz));
@@ -1414,6 +1473,56 @@ int build_step_table(float tau, uint32_t n, uint32_t L, StepRow* rows) {
 // parts (three parts with the specular cone): few blocks per CU, so the tail of
 // the longest waves dominates (a rank of an 8-GPU frame traces 1/8)
 constexpr uint32_t kSplit3MaxBlocks = 1024;   // measured: 3 parts pay off at 1080p / 8 ranks only
+
+// The form of a default-variant launch (K4Tuner in vct_internal.h): 0 = the four-face
+// union form, 1 = the occupancy form.  Timed (counter-free) launches alternate the two
+// until each has kSamples completed samples after its first (cold) one, then the faster
+// one is kept; counting launches take the choice (the union form while timing) and are
+// never timed.  *evp: the event pair to record around a timed launch, or null.
+static int k4_form(vct_ctx* c, uint64_t key, bool timed, hipEvent_t** evp) {
+    K4Tuner& t = c->k4tune;
+    *evp = nullptr;
+    if (t.key != key) {
+        t.key = key;
+        t.chosen = -1;
+        t.since = t.launches = 0;
+        for (int f = 0; f < 2; ++f) { t.seen[f] = 0; t.best[f] = 0.0f; }
+    }
+    if (t.chosen < 0 && timed && t.last) {       // while timing: the previous timed launch first
+        (void)hipEventSynchronize(t.last);
+        t.last = nullptr;
+    }
+    for (int f = 0; f < 2; ++f)                  // harvest completed samples
+        for (int sl = 0; sl < K4Tuner::kSlots; ++sl) {
+            if (!t.busy[f][sl] || hipEventQuery(t.ev[f][sl][1]) != hipSuccess) continue;
+            t.busy[f][sl] = false;
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, t.ev[f][sl][0], t.ev[f][sl][1]) != hipSuccess) continue;
+            if (t.seen[f]++ == 0) continue;      // the first launch of a form pays its code load
+            t.best[f] = t.seen[f] == 2 ? ms : fminf(t.best[f], ms);
+        }
+    if (t.chosen >= 0) {
+        if (!timed || ++t.since < K4Tuner::kRetune) return t.chosen;
+        t.chosen = -1;                           // re-time: the frames may have changed
+        t.since = t.launches = 0;
+        for (int f = 0; f < 2; ++f) { t.seen[f] = 0; t.best[f] = 0.0f; }
+    }
+    if (t.seen[0] > K4Tuner::kSamples && t.seen[1] > K4Tuner::kSamples) {
+        t.chosen = t.best[1] < t.best[0] ? 1 : 0;
+        return t.chosen;
+    }
+    if (!timed) return 0;
+    const int f = (int)(t.launches++ & 1u);
+    const int sl = t.head[f];
+    if (t.busy[f][sl]) return f;                 // every slot of this form in flight: run untimed
+    for (hipEvent_t& e : t.ev[f][sl])
+        if (!e && hipEventCreate(&e) != hipSuccess) return f;
+    t.busy[f][sl] = true;
+    t.head[f] = (sl + 1) % K4Tuner::kSlots;
+    *evp = t.ev[f][sl];
+    t.last = t.ev[f][sl][1];
+    return f;
+}
 
 hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     const Grid& g = c->grid;
@@ -1531,9 +1640,33 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
             if (k.split == 2) hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false, true>), dim3(blocks), dim3(wgs), 0, c->stream, k);
             else hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false>), dim3(blocks), dim3(wgs), 0, c->stream, k);
             break;
-        default:
-            if (counting || !wg1 || (a->variant & 0x4000)) VCT_K4(true, VCT_K4_MIN_WAVES, true);   // 0x4000: counting form
-            else VCT_K4_WG(true, VCT_K4_MIN_WAVES, true, true, false);   // no counters: the timed form
+        default: {
+            // 0x4000: the counting form without counters; 0x1000000 / 0x2000000: the union /
+            // occupancy form (else K4Tuner's choice for this workload)
+            const bool cnt_form = counting || !wg1 || (a->variant & 0x4000);
+            int form;
+            hipEvent_t* ev = nullptr;
+            if (a->variant & 0x1000000) form = 0;
+            else if (a->variant & 0x2000000) form = 1;
+            else {
+                uint64_t key = 1469598103934665603ull;   // FNV-1a over the workload
+                for (uint64_t v : {(uint64_t)a->width, (uint64_t)a->height, (uint64_t)k.rank, (uint64_t)k.world,
+                                   (uint64_t)k.compact, (uint64_t)(k.perm != nullptr), (uint64_t)k.split,
+                                   (uint64_t)c->cfg.n_diffuse, (uint64_t)k.spec_on, (uint64_t)g.n,
+                                   (uint64_t)c->grid_epoch, (uint64_t)(a->variant & 0xffff00u)})
+                    key = (key ^ v) * 1099511628211ull;
+                form = k4_form(c, key, !cnt_form, &ev);
+            }
+            if (ev && hipEventRecord(ev[0], c->stream) != hipSuccess) ev = nullptr;
+            if (cnt_form) {
+                if (form) VCT_K4(true, kOccWaves, false);
+                else VCT_K4(true, VCT_K4_MIN_WAVES, true);
+            } else {
+                if (form) VCT_K4_WG(true, kOccWaves, false, true, false);
+                else VCT_K4_WG(true, VCT_K4_MIN_WAVES, true, true, false);
+            }
+            if (ev) (void)hipEventRecord(ev[1], c->stream);
+        }
     }
 #undef VCT_K4
 #undef VCT_K4_WG

@@ -149,6 +149,12 @@ class Context:
         self._check(self.lib.vct_synchronize(self.h), "synchronize")
 
     @property
+    def trace_form(self) -> int:
+        """Timed form of the default cone trace for the current workload (vct_trace_form):
+        0 four-face union (4 waves/SIMD), 1 occupancy (5 waves/SIMD), -1 still timing."""
+        return int(self.lib.vct_trace_form(self.h))
+
+    @property
     def num_levels(self) -> int:
         return int(self.lib.vct_num_levels(self.h))
 

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("VCT_LIB") or os.path.join(_HERE, "libvct_hip.so")
 # every symbol include/vct.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "vct_create", "vct_destroy", "vct_last_error", "vct_status_string", "vct_abi_version",
-    "vct_get_config", "vct_set_stream", "vct_synchronize", "vct_create_multi", "vct_num_devices", "vct_voxelize", "vct_voxelize_device",
+    "vct_get_config", "vct_set_stream", "vct_synchronize", "vct_create_multi", "vct_num_devices", "vct_trace_form", "vct_voxelize", "vct_voxelize_device",
     "vct_inject_directional", "vct_build_mips", "vct_trace", "vct_trace_device",
     "vct_tiles_for_rank", "vct_untile_device", "vct_untile_planes_device", "vct_untile_planes_packed_device",
     "vct_tile_offset", "vct_comm_get_id", "vct_comm_init", "vct_comm_rank", "vct_comm_broadcast_level0",
@@ -113,6 +113,7 @@ def bind(lib: C.CDLL) -> C.CDLL:
         "vct_synchronize": (i32, [P]),
         "vct_create_multi": (i32, [C.POINTER(VctConfig), u32, C.POINTER(P)]),
         "vct_num_devices": (u32, [P]),
+        "vct_trace_form": (C.c_int32, [P]),
         "vct_voxelize": (i32, [P, P, u32, u32, P, u32, P, P, u32]),
         "vct_voxelize_device": (i32, [P, P, u32, u32, P, u32, P, P, u32]),
         "vct_inject_directional": (i32, [P, C.POINTER(f32), C.POINTER(f32)]),
