@@ -167,7 +167,8 @@ vct_status vct_trace_device(vct_ctx* ctx, const vct_trace_args* args);
 /* The default variant has two bit-identical compiled forms: 0 the four-face-union form
  * (4 waves/SIMD), 1 the occupancy form (5 waves/SIMD, three-face bricks).  The context
  * times both on its first counter-free launches of a workload (frame size, tiling, scene,
- * cone set; HIP events read back without blocking) and keeps the faster one.  Returns the
+ * cone set, G-buffer buffer; while timing, each launch waits for the previous timed one)
+ * and keeps the faster one, re-timing every 4096 launches.  Returns the
  * form of the current workload, or -1 while it is still being timed.  Variant bits
  * 0x1000000 / 0x2000000 force form 0 / 1. */
 int32_t    vct_trace_form(const vct_ctx* ctx);

@@ -1653,7 +1653,8 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
                 for (uint64_t v : {(uint64_t)a->width, (uint64_t)a->height, (uint64_t)k.rank, (uint64_t)k.world,
                                    (uint64_t)k.compact, (uint64_t)(k.perm != nullptr), (uint64_t)k.split,
                                    (uint64_t)c->cfg.n_diffuse, (uint64_t)k.spec_on, (uint64_t)g.n,
-                                   (uint64_t)c->grid_epoch, (uint64_t)(a->variant & 0xffff00u)})
+                                   (uint64_t)c->grid_epoch, (uint64_t)(a->variant & 0xffff00u),
+                                   (uint64_t)(uintptr_t)a->pos4})   // another G-buffer: time again
                     key = (key ^ v) * 1099511628211ull;
                 form = k4_form(c, key, !cnt_form, &ev);
             }
