@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r2}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline --secondary none"}
+BARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline --secondary none --stress none"}
 faulted() { grep -qE "HSA_STATUS_ERROR|Memory access fault|APERTURE_VIOLATION|GPU core dump" "$@"; }
 run() {  # name, rocprof args...
   local name=$1; shift

@@ -9,8 +9,8 @@ TAG=${TAG:-mem}
 OUT=gpurun_out/pmc_mem_$TAG
 mkdir -p $OUT
 [ -n "$LIB" ] && export VCT_LIB=$PWD/voxel-based-global-illumination_amd/$LIB
-KEY="k4_trace<true, 4, true, true, 2, true, false, true, false>"
-BARGS=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline --secondary none"}
+KEY=${KEY:-"k4_trace<true, 5, false, true, 2, true, false, true, false>"}   # the occupancy form (atrium)
+BARGS=${BENCH_ARGS:-"--steps 5 --warmup 1 --no-cpu-baseline --secondary none --stress none"}
 i=0
 for P in ${PASSES:-"GRBM_GUI_ACTIVE TA_TA_BUSY_sum TA_BUSY_avr" "TD_TD_BUSY_sum TD_BUSY_avr" \
     "TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum" \
