@@ -241,15 +241,18 @@ struct LevelView<false> {
     }
 };
 
-// level l (wave-uniform): O32 derives the offset in closed form on the scalar
-// unit (sum of (n >> j)^3 over j = 1 .. l-1 = (n^3 - (n >> (l-1))^3) / 7)
+// level l (wave-uniform): O32 derives the offset in closed form on the scalar unit
+// with shifts only (n a power of two): sum of (n >> j)^3 over j = 1 .. l-1 is the
+// base-8 repunit 1001..001b (l-1 ones) shifted to bit 3 (lg n - l + 1)
 template <bool O32>
 __device__ __forceinline__ LevelView<O32> level_view(const TraceK& k, int l) {
     if constexpr (O32) {
-        const uint32_t n = (uint32_t)k.n, n3 = n * n * n, F = k.aniso ? 6u : 1u;
-        const uint32_t m = n >> (l > 0 ? l - 1 : 0), nl = n >> l;
-        const uint32_t off = l == 0 ? 0u : n3 + F * ((n3 - m * m * m) / 7u);
-        const uint32_t bytes = (l == 0 ? 1u : F) * nl * nl * nl * 16u;
+        const uint32_t lg = (uint32_t)k.lgn, F = k.aniso ? 6u : 1u;
+        const uint32_t S = l == 0 ? 0u
+                                  : (uint32_t)((0x9249249249249249ull & ((1ull << (3u * (uint32_t)(l - 1))) - 1ull))
+                                               << (3u * (lg - (uint32_t)l + 1u)));
+        const uint32_t off = l == 0 ? 0u : (1u << (3u * lg)) + F * S;
+        const uint32_t bytes = (l == 0 ? 1u : F) << (3u * (lg - (uint32_t)l) + 4u);
         return LevelView<true>{__builtin_amdgcn_make_buffer_rsrc((void*)(k.pyr + off), (short)0, (int)bytes,
                                                                  0x00020000)};
     } else {
@@ -692,11 +695,11 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
     if (mode == kIso) {
         t.a = lv.fetch(gi, inb);
     } else {
-        const uint32_t vl = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
-        t.a = lv.fetch((uint32_t)cc.f0 * vl + gi, inb);
-        t.b = lv.fetch((uint32_t)cc.f1 * vl + gi, inb);
-        t.c = lv.fetch((uint32_t)cc.f2 * vl + gi, inb);
-        if (cc.nfaces > 3) t.d = lv.fetch((uint32_t)cc.f3 * vl + gi, inb);
+        const uint32_t sh = 3u * (uint32_t)(k.lgn - l);   // face volume nl^3 = 1 << sh
+        t.a = lv.fetch(((uint32_t)cc.f0 << sh) + gi, inb);
+        t.b = lv.fetch(((uint32_t)cc.f1 << sh) + gi, inb);
+        t.c = lv.fetch(((uint32_t)cc.f2 << sh) + gi, inb);
+        if (cc.nfaces > 3) t.d = lv.fetch(((uint32_t)cc.f3 << sh) + gi, inb);
     }
     return t;
 }
@@ -849,12 +852,13 @@ struct LaneDir {
 // Each level is served from the cache, restaged (both levels' loads in one
 // batch) or, when the wave's footprint does not fit, gathered per lane.
 template <bool O32, bool UNION, int KL>
-__device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx, float qy, float qz, bool active,
-                                              bool two, float fr, const ConeCtl& cc, const LaneDir& ld,
+__device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx, float qy, float qz,
+                                              unsigned long long amA, unsigned long long amB, float fr, const ConeCtl& cc, const LaneDir& ld,
                                               float4* __restrict__ lds, BrickCache& bc, PhaseClock& pc) {
     const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const bool activeB = active && two;
-    const unsigned long long amA = wballot(active), amB = wballot(activeB);
+    // lane masks in SGPRs; the per-lane bools are their inverse ballots (no VGPR round trip)
+    const bool active = __builtin_amdgcn_inverse_ballot_w64(amA);
+    const bool activeB = __builtin_amdgcn_inverse_ballot_w64(amB);
     const bool needB = amB != 0ull;
     const int l1 = l0 + 1;                     // needB implies l0 < L
     const int aniso_mode = cc.dir_uniform ? kComb : kFaces;
@@ -970,12 +974,15 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const bool readA = useA && !bA.zero, readB = useB && !bB.zero;
     if (useA) VCT_DBG(bA.zero ? 17 : 15);          // level-A samples from zero / nonzero bricks
     if (readA || readB) {
-        if (readA && active)
-            sA = brick_sample<KL>(cA, brick_slot(cA, bA, bc.qa), modeA != kFaces, ld.bx(), ld.by(), ld.bz(), ld.wx(),
-                                  ld.wy(), ld.wz(), ldsA);
-        if (readB && activeB)
-            sB = brick_sample<KL>(cB, brick_slot(cB, bB, bc.qb), modeB != kFaces, ld.bx(), ld.by(), ld.bz(), ld.wx(),
-                                  ld.wy(), ld.wz(), ldsB);
+        // every lane samples (no exec-mask branches): an inactive lane reads the brick's
+        // corner-0 texels instead of its own (staged, finite), and its march adds nothing
+        // (march_brick scales the sample by 0)
+        if (readA)
+            sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA, bc.qa) : 0, modeA != kFaces, ld.bx(), ld.by(), ld.bz(),
+                                  ld.wx(), ld.wy(), ld.wz(), ldsA);
+        if (readB)
+            sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB, bc.qb) : 0, modeB != kFaces, ld.bx(), ld.by(),
+                                  ld.bz(), ld.wx(), ld.wy(), ld.wz(), ldsB);
         wave_lds_sync();
     }
     pc.mark(3);
@@ -1082,7 +1089,8 @@ __device__ __forceinline__ void ablate_step(int i) {
     (void)i;
     int s0 = __builtin_amdgcn_readfirstlane(vct_abl_zero()), s1 = s0 + 3;   // not tied to the loop counter
 #pragma unroll
-    for (int j = 0; j < VCT_ABL_SALU / 2; ++j) asm volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1));
+    for (int j = 0; j < VCT_ABL_SALU / 2; ++j)
+        asm volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1) : : "scc");
     asm volatile("" ::"s"(s0), "s"(s1));
 #endif
 #if defined(VCT_ABL_NOP)
@@ -1110,7 +1118,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     const float wdx = dx * dx, wdy = dy * dy, wdz = dz * dz;
     float cr = 0.0f, cg = 0.0f, cb = 0.0f, a = 0.0f, t = 1.0f;
     uint32_t steps = 0;
-    bool active = valid;
+    unsigned long long am = wballot(valid);      // lanes still marching (an SGPR lane mask)
     ConeCtl cc;
     LaneDir ld;
     {
@@ -1129,9 +1137,12 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.f2 = __builtin_ctz(u | 64);
         u &= u - 1;
         cc.f3 = __builtin_ctz(u | 64);
-        ld.blk = (uint32_t)__builtin_popcount(cc.funion & ((1 << fx) - 1)) |
-                 (uint32_t)__builtin_popcount(cc.funion & ((1 << fy) - 1)) << 2 |
-                 (uint32_t)__builtin_popcount(cc.funion & ((1 << fz) - 1)) << 4;
+        // a background lane's faces may lie outside the union (which only the valid lanes
+        // define): it gets block 0, so its (discarded) brick samples read staged texels
+        ld.blk = valid ? (uint32_t)__builtin_popcount(cc.funion & ((1 << fx) - 1)) |
+                             (uint32_t)__builtin_popcount(cc.funion & ((1 << fy) - 1)) << 2 |
+                             (uint32_t)__builtin_popcount(cc.funion & ((1 << fz) - 1)) << 4
+                       : 0u;
         cc.uwx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdx), fl));
         cc.uwy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdy), fl));
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
@@ -1154,11 +1165,17 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
             l0 = __builtin_amdgcn_readlane(tab.l0, i);
         }
         const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
-        // a >= 0.95, t > tmax or outside the grid ends the lane's march (no short-circuit branches)
-        const bool inside = (int)(fminf(fminf(qx, qy), qz) >= 0.0f) & (int)(fmaxf(fmaxf(qx, qy), qz) <= nf);
-        active = active & (a < VCT_ALPHA_STOP) & (t <= k.tmax) & inside;
-        const unsigned long long am = wballot(active);
+        // a >= 0.95, t > tmax or outside the grid ends the lane's march (no short-circuit
+        // branches).  Table rows end with t = +inf: q then has an infinite component (|d| = 1
+        // leaves at most two zero ones, whose NaN min3 / max3 skip), so `inside` already
+        // ends the march there and the t test is only needed for per-lane steps
+        const float qmin = fminf(fminf(qx, qy), qz), qmax = fmaxf(fmaxf(qx, qy), qz);
+        // one ballot per bare compare, ANDed as scalar masks (a ballot of an ANDed i1 goes
+        // through a VGPR)
+        am &= wballot(qmin >= 0.0f) & wballot(qmax <= nf) & wballot(a < VCT_ALPHA_STOP);
+        if constexpr (!TAB) am &= wballot(t <= k.tmax);
         if (am == 0ull) break;
+        const bool active = __builtin_amdgcn_inverse_ballot_w64(am);
         VCT_DBG(TAB ? 36 : 38);                               // wave-steps (table / per-lane steps)
         VCT_DBGN(37, __builtin_popcountll(am));               // active lanes over those wave-steps
         VCT_DBGN(39, __builtin_popcountll(wballot(valid)));   // lanes holding a valid pixel
@@ -1170,13 +1187,18 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
             l0 = (int)m;
             fr = m - (float)l0;
         }
-        const bool two = fr > 0.0f && l0 < k.L;
+        // both levels sampled: fr > 0 (fr >= +0 here, so a nonzero bit pattern) and l0 < L;
+        // for table rows both are wave-uniform: a scalar test, no VALU compare and ballot
+        unsigned long long two_m;
+        if constexpr (TAB) two_m = ((__float_as_uint(fr) != 0u) & (l0 < k.L)) ? ~0ull : 0ull;
+        else two_m = wballot(fr > 0.0f) & wballot(l0 < k.L);
+        const bool two = __builtin_amdgcn_inverse_ballot_w64(two_m);
         const int l0f = TAB ? l0 : __builtin_amdgcn_readlane(l0, __builtin_ctzll(am));
-        float4 s;
+        float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (TAB || wall_in(am, l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
             __builtin_amdgcn_s_setprio(0);       // default priority for the step head, brick geometry and staging
-            s = step_bricks<O32, UNION, KL>(k, l0f, qx, qy, qz, active, two, fr, cc, ld, lds, bc, pc);
+            s = step_bricks<O32, UNION, KL>(k, l0f, qx, qy, qz, am, am & two_m, fr, cc, ld, lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
             s = sample_level<O32, false, gather_chunk<UNION>()>(k, l0, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(),
                                                                   ld.wy(), ld.wz());
@@ -1184,18 +1206,22 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
                 s = blend(s, sample_level<O32, false, gather_chunk<UNION>()>(k, l0 + 1, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(), ld.wy(), ld.wz()),
                           fr);
         }
-        if (active) {
+        // no exec-mask branch: an inactive lane's sample is finite, and with oma = +0 the
+        // fmaf leaves its (c, a) as they are (fmaf(+0, s, c) = c for c >= +0)
+        {
             if constexpr (CNT) {
-                texels += (l0 == 0 || !k.aniso) ? 8u : 24u;
-                if (two) texels += k.aniso ? 24u : 8u;
+                if (active) {
+                    texels += (l0 == 0 || !k.aniso) ? 8u : 24u;
+                    if (two) texels += k.aniso ? 24u : 8u;
+                    ++steps;
+                }
             }
-            const float oma = 1.0f - a;
+            const float oma = active ? 1.0f - a : 0.0f;
             cr = fmaf(oma, s.x, cr);
             cg = fmaf(oma, s.y, cg);
             cb = fmaf(oma, s.z, cb);
             a = fmaf(oma, s.w, a);
-            if constexpr (!TAB) t = t + VCT_STEP_SCALE * D;
-            if constexpr (CNT) ++steps;
+            if constexpr (!TAB) t = t + VCT_STEP_SCALE * D;   // t of a finished lane is never read again
         }
         pc.mark(5);
     }
