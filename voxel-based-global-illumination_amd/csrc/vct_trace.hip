@@ -241,17 +241,14 @@ struct LevelView<false> {
     }
 };
 
-// level l (wave-uniform): O32 derives the offset in closed form on the scalar unit
-// with shifts only (n a power of two): sum of (n >> j)^3 over j = 1 .. l-1 is the
-// base-8 repunit 1001..001b (l-1 ones) shifted to bit 3 (lg n - l + 1)
+// level l (wave-uniform): O32 takes the level's texel offset from the kernel-argument
+// table (one scalar load; measured 0.7-0.9 % faster than deriving it on the scalar unit,
+// which also held ~34 more SGPRs) and its size from shifts (n a power of two)
 template <bool O32>
 __device__ __forceinline__ LevelView<O32> level_view(const TraceK& k, int l) {
     if constexpr (O32) {
         const uint32_t lg = (uint32_t)k.lgn, F = k.aniso ? 6u : 1u;
-        const uint32_t S = l == 0 ? 0u
-                                  : (uint32_t)((0x9249249249249249ull & ((1ull << (3u * (uint32_t)(l - 1))) - 1ull))
-                                               << (3u * (lg - (uint32_t)l + 1u)));
-        const uint32_t off = l == 0 ? 0u : (1u << (3u * lg)) + F * S;
+        const uint32_t off = (uint32_t)k.lvl_off[l];   // < 2^31 texels for n <= 512
         const uint32_t bytes = (l == 0 ? 1u : F) << (3u * (lg - (uint32_t)l) + 4u);
         return LevelView<true>{__builtin_amdgcn_make_buffer_rsrc((void*)(k.pyr + off), (short)0, (int)bytes,
                                                                  0x00020000)};
