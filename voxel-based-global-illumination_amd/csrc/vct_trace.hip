@@ -863,15 +863,12 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const int modeB = k.aniso ? aniso_mode : kIso;
     const bool faces_ok = UNION ? cc.nfaces <= 4 : cc.nfaces == 3;
     if (bc.a.lvl != l0 && bc.b.lvl == l0) {       // the level advanced by one: b becomes a
-        const BrickEntry t = bc.a;
+        // a cone's level never decreases, so the old a (level l0 - 1) is dead: b moves into
+        // a's place, b is emptied and the LDS regions trade roles (no three-way swap)
         bc.a = bc.b;
-        bc.b = t;
+        bc.b.lvl = -1;
         bc.flip ^= 1;
-        if (VCT_QUAD) {
-            const uint32_t q = bc.qa;
-            bc.qa = bc.qb;
-            bc.qb = q;
-        }
+        if (VCT_QUAD) bc.qa = bc.qb;
     }
     float4* ldsA = lds + bc.flip * entry_slots<UNION>();
     float4* ldsB = lds + (bc.flip ^ 1) * entry_slots<UNION>();
