@@ -542,7 +542,6 @@ struct BrickEntry {
     int lvl;                     // staged level (-1 = empty)
     int ox, oy, oz;              // its origin
     int zero;                    // every staged texel is +0: any sample from it is exactly (+0, +0, +0, +0)
-    int quad;                    // four quadrant bricks (origins per lane: BrickCache::qa / qb)
 };
 // The cache holds the bricks of the step's two levels: `a` for level l0, `b`
 // for l0 + 1.  A cone's mip level never decreases, so when l0 advances by one
@@ -552,7 +551,6 @@ struct BrickEntry {
 struct BrickCache {              // wave-uniform, except the quadrant origins
     BrickEntry a, b;
     int flip;                    // 0: a in LDS region 0, b in region 1; 1: swapped
-    uint32_t qa, qb;             // per lane: packed origin of the lane's quadrant brick in a / b (quad entries)
 };
 
 struct Corner {                  // one lane's trilinear footprint at one level
@@ -607,53 +605,6 @@ __device__ __forceinline__ bool brick_origin(const Corner& c, unsigned long long
     b.oy = wave_origin(c.iy, am, fl, (neg >> 1) & 1);
     b.oz = wave_origin(c.iz, am, fl, (neg >> 2) & 1);
     return wall_in(am, in_brick(c, b));
-}
-
-#ifndef VCT_QUAD
-#define VCT_QUAD 0     // measured: A gathers -51 %, K4 +2.3 %
-#endif
-
-// ---------------------------------------------------------------------------
-// Quadrant bricks (iso / comb modes, O32 grids).  With the Morton lane order a
-// 16-lane row of the wave is a 4x4-pixel quadrant.  When the wave's footprint
-// spans more than one 4^3 brick, each quadrant gets its own 4^3 brick in its own
-// block of the entry (the entry holds four blocks for faces mode anyway), and the
-// wave samples all four at once: lane -> block (lane >> 4).  A quadrant's origin
-// is its rows' per-axis minimum (or maximum - 2 toward -axis, the slack ahead of
-// the march), a 16-lane DPP reduction; each lane keeps its quadrant's origin
-// packed in one VGPR (10 bits per axis, bias 4: n <= 512).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int row_min_i32(int v) {   // min over the lane's 16-lane row
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));   // row_half_mirror
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));   // row_mirror
-    return v;
-}
-
-constexpr int kQBias = 4;
-__device__ __forceinline__ int qo_x(uint32_t q) { return (int)(q & 1023u) - kQBias; }
-__device__ __forceinline__ int qo_y(uint32_t q) { return (int)((q >> 10) & 1023u) - kQBias; }
-__device__ __forceinline__ int qo_z(uint32_t q) { return (int)(q >> 20) - kQBias; }
-
-// quadrant origin on one axis (neg: toward -axis); inactive lanes do not count
-__device__ __forceinline__ int quad_axis(int c, bool active, bool neg) {
-    const int v = active ? (neg ? -c : c) : INT_MAX;
-    const int m = row_min_i32(v);
-    return neg ? -m - 2 : m;
-}
-
-// every active lane's footprint inside its quadrant's brick -> packed origin in qo
-__device__ __forceinline__ bool quad_origin(int cx, int cy, int cz, bool active, unsigned long long am, int neg,
-                                            uint32_t& qo) {
-    const int ox = quad_axis(cx, active, neg & 1), oy = quad_axis(cy, active, neg & 2), oz = quad_axis(cz, active, neg & 4);
-    const bool in = max(max((uint32_t)(cx - ox), (uint32_t)(cy - oy)), (uint32_t)(cz - oz)) <= 2u;
-    qo = (uint32_t)(ox + kQBias) | ((uint32_t)(oy + kQBias) << 10) | ((uint32_t)(oz + kQBias) << 20);
-    return (__builtin_amdgcn_ballot_w64(!in) & am) == 0ull;
-}
-
-__device__ __forceinline__ bool in_quad(int cx, int cy, int cz, uint32_t qo) {
-    return max(max((uint32_t)(cx - qo_x(qo)), (uint32_t)(cy - qo_y(qo))), (uint32_t)(cz - qo_z(qo))) <= 2u;
 }
 
 enum { kIso = 0, kComb = 1, kFaces = 2 };
@@ -730,51 +681,8 @@ __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const T
     return nz == 0u;
 }
 
-// the four quadrant bricks of a quad entry (iso / comb): lane j stages texel
-// (j & 3, (j >> 2) & 3, j >> 4) of every quadrant's brick, quadrant q in block q;
-// returns true when every staged value is +0 (the wave's vote)
-template <bool O32>
-__device__ __forceinline__ bool stage_quad(const TraceK& k, int l, int mode, const ConeCtl& cc, uint32_t qo,
-                                           float4* __restrict__ lds) {
-    const int nl = k.n >> l;
-    const int lane = threadIdx.x & 63;
-    const int tx = lane & 3, ty = (lane >> 2) & 3, tz = lane >> 4;
-    const LevelView<O32> lv = level_view<O32>(k, l);
-    const uint32_t vl = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
-    float4* p = lds + ((lane & 15) + kBz * (lane >> 4));
-    uint32_t nz = 0;
-#pragma unroll
-    for (int h = 0; h < 4; h += 2) {
-        float4 v[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)qo, 16 * (h + i));
-            const int sx = qo_x(q) + tx, sy = qo_y(q) + ty, sz = qo_z(q) + tz;
-            const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
-            const uint32_t gi = texel_index((uint32_t)sx, (uint32_t)sy, (uint32_t)sz, (uint32_t)nl);
-            if (mode == kIso) {
-                v[i] = lv.fetch(gi, inb);
-            } else {
-                v[i] = combine3(cc.uwx, cc.uwy, cc.uwz, lv.fetch((uint32_t)cc.f0 * vl + gi, inb),
-                                lv.fetch((uint32_t)cc.f1 * vl + gi, inb), lv.fetch((uint32_t)cc.f2 * vl + gi, inb));
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            p[kBlk * (h + i)] = v[i];
-            nz |= bits4(v[i]);
-        }
-    }
-    return wall(nz == 0u);
-}
-
-// slot of the lane's corner 0 in a staged entry: the wave's brick, or the lane's
-// quadrant brick (block lane >> 4) of a quad entry
-__device__ __forceinline__ int brick_slot(const Corner& c, const BrickEntry& be, uint32_t qo) {
-    if (VCT_QUAD && be.quad) {
-        const int lane = threadIdx.x & 63;
-        return __mul24(kBlk, lane >> 4) + (c.ix - qo_x(qo)) + 4 * (c.iy - qo_y(qo)) + __mul24(kBz, c.iz - qo_z(qo));
-    }
+// slot of the lane's corner 0 in a staged entry
+__device__ __forceinline__ int brick_slot(const Corner& c, const BrickEntry& be) {
     return (c.ix - be.ox) + 4 * (c.iy - be.oy) + __mul24(kBz, c.iz - be.oz);
 }
 
@@ -868,7 +776,6 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         bc.a = bc.b;
         bc.b.lvl = -1;
         bc.flip ^= 1;
-        if (VCT_QUAD) bc.qa = bc.qb;
     }
     float4* ldsA = lds + bc.flip * entry_slots<UNION>();
     float4* ldsB = lds + (bc.flip ^ 1) * entry_slots<UNION>();
@@ -876,10 +783,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // level A: cached, restaged, or gathered
     const Corner cA = level_corner(l0, qx, qy, qz);
     BrickEntry bA = bc.a;
-    const auto fits = [&](const Corner& c, const BrickEntry& be, uint32_t qo) {
-        return (VCT_QUAD && be.quad) ? in_quad(c.ix, c.iy, c.iz, qo) : in_brick(c, be);
-    };
-    bool useA = bA.lvl == l0 && wall_in(amA, fits(cA, bA, bc.qa));
+    bool useA = bA.lvl == l0 && wall_in(amA, in_brick(cA, bA));
     bool stA = false;
     if (!useA && (modeA != kFaces || faces_okA)) {
         BrickEntry nb{};
@@ -888,15 +792,6 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
             bA = nb;
             bc.a = nb;
             useA = stA = true;
-        } else if (VCT_QUAD && O32 && UNION && modeA != kFaces) {   // one brick per quadrant (four blocks: UNION entries)
-            uint32_t q;
-            if (quad_origin(cA.ix, cA.iy, cA.iz, active, amA, cc.neg, q)) {
-                nb.quad = 1;
-                bA = nb;
-                bc.a = nb;
-                bc.qa = q;
-                useA = stA = true;
-            }
         }
     }
     Corner cB = cA;
@@ -904,7 +799,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     bool useB = false, stB = false;
     if (needB) {
         cB = level_corner(l1, qx, qy, qz);
-        useB = bB.lvl == l1 && wall_in(amB, fits(cB, bB, bc.qb));
+        useB = bB.lvl == l1 && wall_in(amB, in_brick(cB, bB));
         if (!useB && (modeB != kFaces || faces_okB)) {
             BrickEntry nb{};
             nb.lvl = l1;
@@ -912,20 +807,9 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
                 bB = nb;
                 bc.b = nb;
                 useB = stB = true;
-            } else if (VCT_QUAD && O32 && UNION && modeB != kFaces) {
-                uint32_t q;
-                if (quad_origin(cB.ix, cB.iy, cB.iz, activeB, amB, cc.neg, q)) {
-                    nb.quad = 1;
-                    bB = nb;
-                    bc.b = nb;
-                    bc.qb = q;
-                    useB = stB = true;
-                }
             }
         }
     }
-    if (useA && bA.quad) VCT_DBG(stA ? 32 : 33);
-    if (useB && bB.quad) VCT_DBG(stB ? 34 : 35);
     VCT_DBG(useA ? (stA ? 2 : 3) : 1);
     VCT_DBG(needB ? (useB ? (stB ? 27 : 26) : 28) : 31);   // level B: hit / staged / gathered / not sampled
     if (useA && modeA == kFaces) VCT_DBG(29);               // brick samples read three faces per corner
@@ -934,19 +818,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // a brick whose texels are all +0 (empty space) is marked: its samples are exactly
     // zero (fmaf(w, +0, +0) = +0 through the whole trilinear chain), so hits on it skip
     // the LDS reads and the FMAs
-    if (VCT_QUAD && ((stA && bA.quad) || (stB && bB.quad))) {   // a quad entry: stage the levels one by one
-        if (stA) {
-            const bool z = bA.quad ? stage_quad<O32>(k, l0, modeA, cc, bc.qa, ldsA)
-                                   : wall(stage_store(modeA, cc, stage_load<O32>(k, l0, bA, modeA, cc), ldsA));
-            bA.zero = bc.a.zero = z;
-        }
-        if (stB) {
-            const bool z = bB.quad ? stage_quad<O32>(k, l1, modeB, cc, bc.qb, ldsB)
-                                   : wall(stage_store(modeB, cc, stage_load<O32>(k, l1, bB, modeB, cc), ldsB));
-            bB.zero = bc.b.zero = z;
-        }
-        wave_lds_sync();
-    } else if (stA && stB) {
+    if (stA && stB) {
         const Tex4 tA = stage_load<O32>(k, l0, bA, modeA, cc);
         const Tex4 tB = stage_load<O32>(k, l1, bB, modeB, cc);
         const bool zA = stage_store(modeA, cc, tA, ldsA);
@@ -972,10 +844,10 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         // corner-0 texels instead of its own (staged, finite), and its march adds nothing
         // (march_brick scales the sample by 0)
         if (readA)
-            sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA, bc.qa) : 0, modeA != kFaces, ld.bx(), ld.by(), ld.bz(),
+            sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA) : 0, modeA != kFaces, ld.bx(), ld.by(), ld.bz(),
                                   ld.wx(), ld.wy(), ld.wz(), ldsA);
         if (readB)
-            sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB, bc.qb) : 0, modeB != kFaces, ld.bx(), ld.by(),
+            sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB) : 0, modeB != kFaces, ld.bx(), ld.by(),
                                   ld.bz(), ld.wx(), ld.wy(), ld.wz(), ldsB);
         wave_lds_sync();
     }
@@ -1144,9 +1016,8 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.dir_uniform = wall_in(vm, (wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz)) && cc.nfaces == 3;
     }
     BrickCache bc;
-    bc.a = bc.b = BrickEntry{-1, 0, 0, 0, 0, 0};
+    bc.a = bc.b = BrickEntry{-1, 0, 0, 0, 0};
     bc.flip = 0;
-    bc.qa = bc.qb = 0u;
     for (int i = 0;; ++i) {
         asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz), "+v"(ld.blk));   // see LaneDir
         ld.dx = dx; ld.dy = dy; ld.dz = dz;
