@@ -835,7 +835,10 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         wave_lds_sync();
     }
     pc.mark(2);
-    __builtin_amdgcn_s_setprio(3);               // LDS sampling / FMAs issue ahead of other waves (A/B: -0.6 %)
+#ifndef VCT_K4_PRIO
+#define VCT_K4_PRIO 3
+#endif
+    if (VCT_K4_PRIO) __builtin_amdgcn_s_setprio(VCT_K4_PRIO);   // LDS sampling / FMAs issue ahead of other waves (A/B: -0.6 %)
     float4 sA = z4, sB = z4;
     const bool readA = useA && !bA.zero, readB = useB && !bB.zero;
     if (useA) VCT_DBG(bA.zero ? 17 : 15);          // level-A samples from zero / nonzero bricks
@@ -1062,7 +1065,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (TAB || wall_in(am, l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
-            __builtin_amdgcn_s_setprio(0);       // default priority for the step head, brick geometry and staging
+            if (VCT_K4_PRIO) __builtin_amdgcn_s_setprio(0);   // default priority for the step head, brick geometry and staging
             s = step_bricks<O32, UNION, KL>(k, l0f, qx, qy, qz, am, am & two_m, fr, cc, ld, lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
             s = sample_level<O32, false, gather_chunk<UNION>()>(k, l0, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(),
@@ -1373,11 +1376,15 @@ constexpr uint32_t kSplit3MaxBlocks = 1024;   // measured: 3 parts pay off at 10
 static int k4_form(vct_ctx* c, uint64_t key, bool timed, hipEvent_t** evp) {
     K4Tuner& t = c->k4tune;
     *evp = nullptr;
-    if (t.key != key) {
+    if (t.key != key) {                          // a new workload: its samples start afresh
         t.key = key;
         t.chosen = -1;
         t.since = t.launches = 0;
-        for (int f = 0; f < 2; ++f) { t.seen[f] = 0; t.best[f] = 0.0f; }
+        for (int f = 0; f < 2; ++f) {
+            t.seen[f] = 0;
+            t.best[f] = 0.0f;
+            for (bool& b : t.busy[f]) b = false; // launches of the old workload still in flight: not its samples
+        }
     }
     if (t.chosen < 0 && timed && t.last) {       // while timing: the previous timed launch first
         (void)hipEventSynchronize(t.last);
