@@ -497,8 +497,9 @@ def settle_form(ctx, torch, launch, max_launches=24):
 
 def stress_rand(args, torch, ctx, dev, stream):
     """G_rand (independent random surface points and normals per pixel) on the
-    scene in `ctx`: the K4 pass in screen order and with ray reordering (variant 0x8000),
-    timed alike; both must be bit-identical."""
+    scene in `ctx`: the K4 pass in screen order (0x4000000), with ray reordering (0x8000)
+    and as the default variant chooses (the tuner times both orders), timed alike; all
+    must be bit-identical."""
     from vct import scenes
     from vct.camera import Camera
     w, h = args.width, args.height
@@ -510,10 +511,11 @@ def stress_rand(args, torch, ctx, dev, stream):
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     outs, ms, form = {}, {}, {}
     reps = max(3, args.steps // 4)
-    for v in (args.variant & ~0x8000, args.variant | 0x8000):
+    auto = args.variant & ~0x4008000
+    for v in (auto | 0x4000000, auto | 0x8000, auto):   # screen order forced / reordering forced / tuner's choice
         d = torch.empty((h, w, 4), device=dev)
         sp = torch.empty((h, w, 4), device=dev)
-        if v & 0x8000 == 0:
+        if v & 0x4000000:      # the counting pass, once (screen order)
             ctx.trace_device(*gb, w, h, eye, d, sp, cone_steps=cnt, variant=v)
         form[v] = settle_form(ctx, torch, lambda: ctx.trace_device(*gb, w, h, eye, d, sp, variant=v))
         ctx.trace_device(*gb, w, h, eye, d, sp, variant=v)     # warm
@@ -527,14 +529,17 @@ def stress_rand(args, torch, ctx, dev, stream):
         ms[v] = e[0].elapsed_time(e[1]) / reps
         outs[v] = (d, sp)
     steps = int(cnt[0].item())
-    (a0, a1), (b0, b1) = outs.values()
-    t0, t1 = ms.values()
+    (a0, a1), (b0, b1), (c0, c1) = outs.values()
+    t0, t1, t2 = ms.values()
     return {"gbuffer": "G_rand (seed 42), same grid", "frame_cone_steps": steps, "frames": reps,
-            "screen_order_ms": round(t0, 4), "reordered_ms": round(t1, 4),
+            "screen_order_ms": round(t0, 4), "reordered_ms": round(t1, 4), "default_ms": round(t2, 4),
             "screen_order_Mcone_steps_s": round(steps / t0 / 1e3, 2),
             "reordered_Mcone_steps_s": round(steps / t1 / 1e3, 2),
+            "default_Mcone_steps_s": round(steps / t2 / 1e3, 2),
             "speedup": round(t0 / t1, 3), "k4_forms": list(form.values()),
-            "bitexact": bool(torch.equal(a0, b0) and torch.equal(a1, b1))}
+            "default_choice": "ray reordering" if form[auto] >= 0 and form[auto] & 2 else "screen order",
+            "bitexact": bool(torch.equal(a0, b0) and torch.equal(a1, b1) and torch.equal(a0, c0) and
+                             torch.equal(a1, c1))}
 
 
 def run(args, world):
@@ -598,7 +603,9 @@ def run(args, world):
             result[k_] = m[k_]
         result["k4_kernel_ms_avg"] = round(m["k4_kernel_ms_avg"], 4)
         result["k4_kernel_ms_median"] = round(m["k4_kernel_ms_median"], 4)
-        result["k4_form"] = {0: "four-face union, 4 waves/SIMD", 1: "occupancy, 5 waves/SIMD"}.get(m["k4_form"], None)
+        f = m["k4_form"]
+        result["k4_form"] = None if f < 0 else ("occupancy, 5 waves/SIMD" if f & 1 else "four-face union, 4 waves/SIMD") + (
+            ", ray reordering" if f & 2 else ", screen order")
         for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
                    "frame_relight_bcast_ms", "frame_relight_replicated_ms", "replicated_k2_equals_bcast",
                    "trace_ms_max_rank", "gather_ms", "allgather_ms"):

@@ -164,13 +164,16 @@ vct_status vct_trace(vct_ctx* ctx, const float* gbuf_pos4, const float* gbuf_nrm
                      uint32_t* out_steps_px, uint64_t* out_cone_steps);
 /* Device-resident form (asynchronous on the ctx stream). */
 vct_status vct_trace_device(vct_ctx* ctx, const vct_trace_args* args);
-/* The default variant has two bit-identical compiled forms: 0 the four-face-union form
- * (4 waves/SIMD), 1 the occupancy form (5 waves/SIMD, three-face bricks).  The context
- * times both on its first counter-free launches of a workload (frame size, tiling, scene,
- * cone set, G-buffer buffer; while timing, each launch waits for the previous timed one)
- * and keeps the faster one, re-timing every 4096 launches.  Returns the
- * form of the current workload, or -1 while it is still being timed.  Variant bits
- * 0x1000000 / 0x2000000 force form 0 / 1. */
+/* The default variant has two bit-identical compiled forms, the four-face-union form
+ * (4 waves/SIMD) and the occupancy form (5 waves/SIMD, three-face bricks), and a one-rank
+ * full frame can be traced in screen order or with ray reordering (0x8000).  The context
+ * times the candidates the variant leaves open on its first counter-free launches of a
+ * workload (frame size, tiling, scene, cone set, G-buffer buffer; while timing, each
+ * launch waits for the previous timed one) and keeps the fastest, re-timing every 4096
+ * launches.  Returns the kept candidate of the current workload -- bit 0 the form
+ * (0 union, 1 occupancy), bit 1 ray reordering -- or -1 while it is still being timed.
+ * Variant bits 0x1000000 / 0x2000000 force the union / occupancy form, 0x8000 / 0x4000000
+ * ray reordering / screen order. */
 int32_t    vct_trace_form(const vct_ctx* ctx);
 /* Number of 64x64 tiles rank `rank` of `world` traces for a width x height frame. */
 uint32_t   vct_tiles_for_rank(uint32_t width, uint32_t height, uint32_t rank, uint32_t world);

@@ -57,7 +57,7 @@ def main():
         for _ in range(24):
             ctx.trace_device(*gb, a.w, a.h, cam.position, *outs[v], variant=v)
             torch.cuda.synchronize()
-            if v & 0x3000000 or ctx.trace_form >= 0:
+            if (v & 0x3000000 and v & 0x4008000) or ctx.trace_form >= 0:
                 break
     for _ in range(a.rounds):
         for v in variants:

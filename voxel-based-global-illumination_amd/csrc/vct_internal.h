@@ -45,10 +45,12 @@ struct Scratch {
     size_t bytes = 0;
 };
 
-// K4 form choice (vct_trace.hip k4_form).  The default cone trace has two bit-identical
-// compiled forms: the four-face-union form (4 waves/SIMD; pays on curved surfaces, where
-// a wave's lanes straddle an axis) and the occupancy form (5 waves/SIMD, three-face
-// bricks; pays on flat ones).  A context times both on its first timed launches of a
+// K4 candidate choice (vct_trace.hip k4_form).  The default cone trace has two
+// bit-identical compiled forms: the four-face-union form (4 waves/SIMD; pays on curved
+// surfaces, where a wave's lanes straddle an axis) and the occupancy form (5 waves/SIMD,
+// three-face bricks; pays on flat ones); a one-rank full frame may also be traced in
+// screen order or with ray reordering (pays on incoherent G-buffers).  Candidate
+// c = form | reordered << 1, over the dimensions the variant leaves free.  A context times both on its first timed launches of a
 // workload (HIP events on its stream; while timing, a launch first waits for the previous
 // timed one to finish, so the choice is made within 7 launches even when the host queues
 // frames far ahead), keeps the faster one, and re-times after kRetune launches or when
@@ -58,14 +60,14 @@ struct K4Tuner {
     static constexpr int kSamples = 2;        // timed samples per form after the first (cold) one
     static constexpr uint32_t kRetune = 4096;
     uint64_t key = ~0ull;                     // workload the state belongs to
-    int chosen = -1;                          // 0 union form, 1 occupancy form; -1 still timing
+    int chosen = -1;                          // the candidate kept; -1 still timing
     uint32_t since = 0;                       // timed launches since the choice
     uint32_t launches = 0;                    // timed launches while choosing
-    hipEvent_t ev[2][kSlots][2] = {};
-    bool busy[2][kSlots] = {};
-    int head[2] = {0, 0};
-    int seen[2] = {0, 0};                     // completed samples (the first one is dropped)
-    float best[2] = {0.0f, 0.0f};             // fastest completed sample, ms
+    hipEvent_t ev[4][kSlots][2] = {};
+    bool busy[4][kSlots] = {};
+    int head[4] = {0, 0, 0, 0};
+    int seen[4] = {0, 0, 0, 0};               // completed samples (the first one is dropped)
+    float best[4] = {0.0f, 0.0f, 0.0f, 0.0f}; // fastest completed sample, ms
     hipEvent_t last = nullptr;                // end event of the previous timed launch while timing
 };
 

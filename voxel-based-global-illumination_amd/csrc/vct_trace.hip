@@ -1368,19 +1368,21 @@ int build_step_table(float tau, uint32_t n, uint32_t L, StepRow* rows) {
 // the longest waves dominates (a rank of an 8-GPU frame traces 1/8)
 constexpr uint32_t kSplit3MaxBlocks = 1024;   // measured: 3 parts pay off at 1080p / 8 ranks only
 
-// The form of a default-variant launch (K4Tuner in vct_internal.h): 0 = the four-face
-// union form, 1 = the occupancy form.  Timed (counter-free) launches alternate the two
-// until each has kSamples completed samples after its first (cold) one, then the faster
-// one is kept; counting launches take the choice (the union form while timing) and are
-// never timed.  *evp: the event pair to record around a timed launch, or null.
-static int k4_form(vct_ctx* c, uint64_t key, bool timed, hipEvent_t** evp) {
+// The candidate of a default-variant launch (K4Tuner in vct_internal.h): bit 0 the
+// form (0 union, 1 occupancy), bit 1 ray reordering.  cands lists the candidates the
+// variant leaves open (n of them, 1, 2 or 4).  Timed (counter-free) launches cycle
+// through them until each has kSamples completed samples after its first (cold) one,
+// then the fastest is kept; counting launches take the choice (cands[0] while timing)
+// and are never timed.  *evp: the event pair to record around a timed launch, or null.
+static int k4_form(vct_ctx* c, uint64_t key, const int* cands, int n, bool timed, hipEvent_t** evp) {
     K4Tuner& t = c->k4tune;
     *evp = nullptr;
+    if (n == 1) return cands[0];
     if (t.key != key) {                          // a new workload: its samples start afresh
         t.key = key;
         t.chosen = -1;
         t.since = t.launches = 0;
-        for (int f = 0; f < 2; ++f) {
+        for (int f = 0; f < 4; ++f) {
             t.seen[f] = 0;
             t.best[f] = 0.0f;
             for (bool& b : t.busy[f]) b = false; // launches of the old workload still in flight: not its samples
@@ -1390,29 +1392,34 @@ static int k4_form(vct_ctx* c, uint64_t key, bool timed, hipEvent_t** evp) {
         (void)hipEventSynchronize(t.last);
         t.last = nullptr;
     }
-    for (int f = 0; f < 2; ++f)                  // harvest completed samples
+    for (int f = 0; f < 4; ++f)                  // harvest completed samples
         for (int sl = 0; sl < K4Tuner::kSlots; ++sl) {
             if (!t.busy[f][sl] || hipEventQuery(t.ev[f][sl][1]) != hipSuccess) continue;
             t.busy[f][sl] = false;
             float ms = 0.0f;
             if (hipEventElapsedTime(&ms, t.ev[f][sl][0], t.ev[f][sl][1]) != hipSuccess) continue;
-            if (t.seen[f]++ == 0) continue;      // the first launch of a form pays its code load
+            if (t.seen[f]++ == 0) continue;      // the first launch of a candidate pays its code load
             t.best[f] = t.seen[f] == 2 ? ms : fminf(t.best[f], ms);
         }
     if (t.chosen >= 0) {
         if (!timed || ++t.since < K4Tuner::kRetune) return t.chosen;
         t.chosen = -1;                           // re-time: the frames may have changed
         t.since = t.launches = 0;
-        for (int f = 0; f < 2; ++f) { t.seen[f] = 0; t.best[f] = 0.0f; }
+        for (int f = 0; f < 4; ++f) { t.seen[f] = 0; t.best[f] = 0.0f; }
     }
-    if (t.seen[0] > K4Tuner::kSamples && t.seen[1] > K4Tuner::kSamples) {
-        t.chosen = t.best[1] < t.best[0] ? 1 : 0;
+    bool done = true;
+    for (int i = 0; i < n; ++i) done = done && t.seen[cands[i]] > K4Tuner::kSamples;
+    if (done) {
+        int b = cands[0];
+        for (int i = 1; i < n; ++i)
+            if (t.best[cands[i]] < t.best[b]) b = cands[i];
+        t.chosen = b;
         return t.chosen;
     }
-    if (!timed) return 0;
-    const int f = (int)(t.launches++ & 1u);
+    if (!timed) return cands[0];
+    const int f = cands[t.launches++ % (uint32_t)n];
     const int sl = t.head[f];
-    if (t.busy[f][sl]) return f;                 // every slot of this form in flight: run untimed
+    if (t.busy[f][sl]) return f;                 // every slot of this candidate in flight: run untimed
     for (hipEvent_t& e : t.ev[f][sl])
         if (!e && hipEventCreate(&e) != hipSuccess) return f;
     t.busy[f][sl] = true;
@@ -1469,7 +1476,41 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.npx = a->width * a->height;
     uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
-    if ((a->variant & 0x8000) && world == 1 && !k.compact) {
+    const bool counting = k.steps_px || k.steps_total || k.texels_total;
+    // Default variant: the form (bits 0x1000000 / 0x2000000 force union / occupancy) and,
+    // for a one-rank full frame, the ray order (0x8000 forces reordering, 0x4000000 screen
+    // order) that the bits leave open are chosen by the tuner (k4_form).  Other variants:
+    // reordering only when 0x8000 asks for it.
+    const bool deflt = (a->variant & 0xff) == 0;
+    const bool can_reorder = world == 1 && !k.compact;
+    const bool cnt_form = counting || (a->variant & 0x1000) || (a->variant & 0x4000);   // 0x1000: four waves per workgroup
+    int cand = 0;
+    hipEvent_t* ev = nullptr;
+    {
+        int forms[2], nf = 0, orders[2], no = 0;
+        if (a->variant & 0x1000000) forms[nf++] = 0;
+        else if (a->variant & 0x2000000) forms[nf++] = 1;
+        else { forms[nf++] = 0; forms[nf++] = 1; }
+        if (!can_reorder || (a->variant & 0x4000000)) orders[no++] = 0;
+        else if ((a->variant & 0x8000) || !deflt) orders[no++] = (a->variant & 0x8000) ? 1 : 0;
+        else { orders[no++] = 0; orders[no++] = 1; }
+        if (deflt) {
+            int cands[4], n = 0;
+            for (int o = 0; o < no; ++o)
+                for (int f = 0; f < nf; ++f) cands[n++] = forms[f] | orders[o] << 1;
+            uint64_t key = 1469598103934665603ull;   // FNV-1a over the workload
+            for (uint64_t v : {(uint64_t)a->width, (uint64_t)a->height, (uint64_t)k.rank, (uint64_t)k.world,
+                               (uint64_t)k.compact, (uint64_t)k.split, (uint64_t)c->cfg.n_diffuse, (uint64_t)k.spec_on,
+                               (uint64_t)g.n, (uint64_t)c->grid_epoch, (uint64_t)(a->variant & 0x7ffff00u),
+                               (uint64_t)(uintptr_t)a->pos4})   // another G-buffer: time again
+                key = (key ^ v) * 1099511628211ull;
+            cand = k4_form(c, key, cands, n, !cnt_form, &ev);
+        } else {
+            cand = orders[0] << 1;
+        }
+    }
+    if (ev && hipEventRecord(ev[0], c->stream) != hipSuccess) ev = nullptr;
+    if (cand & 2) {
         // ray reordering (full frame, one rank): waves take 64 consecutive entries of the
         // sorted pixel list; nlt counts 64-wave units of it instead of 64x64 tiles
         hipError_t e = launch_reorder(c, a, &k.perm);
@@ -1514,7 +1555,6 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         const uint32_t unit_g = wg1 ? 1u : 4u;      // a 16x16 block is 4 waves
         k.xcd_g = (int)((units_per_part * unit_g >= 16384u ? 64u : 16u) / unit_g);
     }
-    const bool counting = k.steps_px || k.steps_total || k.texels_total;
     // O32 instantiations need every level below 4 GiB: n <= 512
     const bool o32 = g.n <= 512;
 #define VCT_K4_WG(BRICK, MINW, UNION, WG, CNT)                                                          \
@@ -1539,24 +1579,8 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
             else hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false>), dim3(blocks), dim3(wgs), 0, c->stream, k);
             break;
         default: {
-            // 0x4000: the counting form without counters; 0x1000000 / 0x2000000: the union /
-            // occupancy form (else K4Tuner's choice for this workload)
-            const bool cnt_form = counting || !wg1 || (a->variant & 0x4000);
-            int form;
-            hipEvent_t* ev = nullptr;
-            if (a->variant & 0x1000000) form = 0;
-            else if (a->variant & 0x2000000) form = 1;
-            else {
-                uint64_t key = 1469598103934665603ull;   // FNV-1a over the workload
-                for (uint64_t v : {(uint64_t)a->width, (uint64_t)a->height, (uint64_t)k.rank, (uint64_t)k.world,
-                                   (uint64_t)k.compact, (uint64_t)(k.perm != nullptr), (uint64_t)k.split,
-                                   (uint64_t)c->cfg.n_diffuse, (uint64_t)k.spec_on, (uint64_t)g.n,
-                                   (uint64_t)c->grid_epoch, (uint64_t)(a->variant & 0xffff00u),
-                                   (uint64_t)(uintptr_t)a->pos4})   // another G-buffer: time again
-                    key = (key ^ v) * 1099511628211ull;
-                form = k4_form(c, key, !cnt_form, &ev);
-            }
-            if (ev && hipEventRecord(ev[0], c->stream) != hipSuccess) ev = nullptr;
+            // 0x4000: the counting form without counters; the form is the candidate's bit 0
+            const int form = cand & 1;
             if (cnt_form) {
                 if (form) VCT_K4(true, kOccWaves, false);
                 else VCT_K4(true, VCT_K4_MIN_WAVES, true);

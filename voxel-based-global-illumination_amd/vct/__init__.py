@@ -150,8 +150,9 @@ class Context:
 
     @property
     def trace_form(self) -> int:
-        """Timed form of the default cone trace for the current workload (vct_trace_form):
-        0 four-face union (4 waves/SIMD), 1 occupancy (5 waves/SIMD), -1 still timing."""
+        """Kept candidate of the default cone trace for the current workload (vct_trace_form):
+        bit 0 the form (0 four-face union, 4 waves/SIMD; 1 occupancy, 5 waves/SIMD), bit 1
+        ray reordering; -1 while still timing."""
         return int(self.lib.vct_trace_form(self.h))
 
     @property
