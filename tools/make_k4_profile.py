@@ -25,26 +25,29 @@ TIMED = re.compile(r"k4_trace<[^>]*, false>\(")
 
 
 def per_kernel(d):
-    """Mean per dispatch of every counter for the timed K4 form the run used most.  The
-    default variant has two timed forms (k4_trace<..., 4, true, ...> union and <..., 5,
-    false, ...> occupancy); the context times both on its first launches, then keeps one,
-    so the most-dispatched form is the one the bench measured."""
+    """Mean per dispatch of every counter for the timed K4 launch shape the run used most.
+    The default variant's tuner times several candidates on its first launches (two
+    compiled forms, k4_trace<..., 4, true, ...> union and <..., 5, false, ...> occupancy,
+    and for one-rank frames screen order or ray reordering, which changes the grid), then
+    keeps one; so the most frequent (kernel, grid size) pair is what the bench measured."""
     vals, durs = {}, {}
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 if TIMED.search(r["Kernel_Name"]):
-                    durs.setdefault(r["Kernel_Name"], []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                    key = (r["Kernel_Name"], int(r["Grid_Size_X"]))
+                    durs.setdefault(key, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 if TIMED.search(r["Kernel_Name"]):
-                    vals.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], []).append(
-                        float(r["Counter_Value"]))
-    name = max(durs, key=lambda k: len(durs[k])) if durs else None
-    out = {k: sum(v) / len(v) for k, v in sorted(vals.get(name, {}).items())}
-    dd = durs.get(name, [])
-    out["kernel"] = name
+                    key = (r["Kernel_Name"], int(r["Grid_Size"]))
+                    vals.setdefault(key, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    key = max(durs, key=lambda k: len(durs[k])) if durs else None
+    out = {k: sum(v) / len(v) for k, v in sorted(vals.get(key, {}).items())}
+    dd = durs.get(key, [])
+    out["kernel"] = key[0] if key else None
+    out["grid_threads"] = key[1] if key else None
     out["dispatches"] = len(dd)
     out["duration_ms"] = sum(dd) / len(dd) / 1e6 if dd else None
     return out
