@@ -545,10 +545,10 @@ struct BrickEntry {
 };
 // The cache holds the bricks of the step's two levels: `a` for level l0, `b`
 // for l0 + 1.  A cone's mip level never decreases, so when l0 advances by one
-// the old `b` becomes the new `a` (the two swap, with their LDS regions) and
+// the old `b` becomes the new `a` (b moves in, the LDS regions trade roles) and
 // `b` restages; no per-step indexing (a runtime-indexed pair would cost
 // scalar selects on every access).
-struct BrickCache {              // wave-uniform, except the quadrant origins
+struct BrickCache {              // wave-uniform
     BrickEntry a, b;
     int flip;                    // 0: a in LDS region 0, b in region 1; 1: swapped
 };
