@@ -149,6 +149,38 @@ vct_status vct_voxelize_device(vct_ctx* ctx, const void* verts, uint32_t vertex_
                                const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_material,
                                const float* material_kd4, uint32_t n_materials);
 
+/* ---- diffuse maps: albedo = Kd x map (SURVEY.md 8a Model::loadMaterials) -----
+ * Replaces what Model::loadMaterialTextures / TextureFromFile (model.cpp:150-226)
+ * hand to GL: stbi_load'ed images uploaded with glTexImage2D and sampled with
+ * GL_REPEAT / GL_LINEAR (model.cpp:212-216).  A texture is width x height RGBA8
+ * texels, row 0 = the image's first row (stbi_load order = GL's t = 0 row); a host
+ * loader expands 1- / 3-channel images as GL_RED / GL_RGB sample them, (r,0,0,255) /
+ * (r,g,b,255).  Sampling rule, UV of a voxel hit and of a G-buffer hit: vct_spec.h
+ * "diffuse maps". */
+typedef struct vct_texture {
+    const uint8_t* rgba8;  /* host, width * height * 4 bytes                  */
+    uint32_t width, height;/* 1 .. VCT_TEX_MAX_DIM                            */
+} vct_texture;
+/* Uploads the textures to the device, replacing the previous set (n_textures = 0
+ * clears it).  Synchronous.  The G-buffer passes sample the set current at their call. */
+vct_status vct_set_textures(vct_ctx* ctx, const vct_texture* textures, uint32_t n_textures);
+/* K1 with diffuse maps.  As vct_voxelize, plus: material_map[m] = the vct_set_textures
+ * index of material m's diffuse map, or -1 (albedo = Kd); uv_offset = byte offset of the
+ * two TexCoords floats in a vertex record (24 in the reference Vertex, stdafx.h:36-42,
+ * mesh.cpp:49).  A mapped material's triangle contributes albedo = Kd x T(uv) per covered
+ * voxel; vct_gbuffer_raycast_device / vct_gbuffer_raster_device then write albedo =
+ * Kd x T(uv of the hit).  material_map needs n_materials entries; out-of-range entries
+ * are VCT_EINVAL. */
+vct_status vct_voxelize_textured(vct_ctx* ctx, const void* verts, uint32_t vertex_stride, uint32_t n_verts,
+                                 const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_material,
+                                 const float* material_kd4, const int32_t* material_map, uint32_t n_materials,
+                                 uint32_t uv_offset);
+/* Same on device-resident arrays (material_map 4-byte aligned); see vct_voxelize_device. */
+vct_status vct_voxelize_textured_device(vct_ctx* ctx, const void* verts, uint32_t vertex_stride, uint32_t n_verts,
+                                        const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_material,
+                                        const float* material_kd4, const int32_t* material_map,
+                                        uint32_t n_materials, uint32_t uv_offset);
+
 /* ---- K2 direct-light injection (A.3) ----------------------------------- */
 vct_status vct_inject_directional(vct_ctx* ctx, const float dir_to_light[3], const float color[3]);
 

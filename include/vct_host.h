@@ -10,6 +10,7 @@
  */
 #ifndef VCT_HOST_H
 #define VCT_HOST_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -27,6 +28,23 @@ int vcth_mesh(const vcth_model* m, uint32_t i, const void** verts, uint32_t* n_v
               uint32_t* n_idx, uint32_t* material);
 /* Material i: name, Ka/Kd/Ks (r, g, b, 1). */
 int vcth_material(const vcth_model* m, uint32_t i, const char** name, float ka[4], float kd[4], float ks[4]);
+/* Material i's diffuse map: the map_Kd path of the .mtl ("" = none) and its index in
+ * the model's texture list (-1: none, or it failed to load).  The model loads each
+ * diffuse map once per path (Model::loadMaterialTextures, model.cpp:150-186). */
+int vcth_material_diffuse_map(const vcth_model* m, uint32_t i, const char** path, int32_t* texture);
+uint32_t vcth_num_textures(const vcth_model* m);
+/* Texture i: RGBA8 texels (row 0 = the image's top row, 1/3-channel images expanded as
+ * GL_RED / GL_RGB sample), size, .mtl path: the vct_texture of vct_set_textures. */
+int vcth_texture(const vcth_model* m, uint32_t i, const uint8_t** rgba8, uint32_t* width, uint32_t* height,
+                 const char** path);
+/* Maps that failed to load, "path: reason" (TextureFromFile prints them, model.cpp:219-223). */
+uint32_t vcth_num_texture_errors(const vcth_model* m);
+const char* vcth_texture_error(const vcth_model* m, uint32_t i);
+/* PNG decode as stbi_load(file, &w, &h, &comp, 0) (model.cpp:197): *data = h rows of
+ * w * comp bytes (release with vcth_free_image).  Returns 0, or -1 with a message. */
+int vcth_decode_png(const uint8_t* file, size_t bytes, uint8_t** data, uint32_t* width, uint32_t* height, int* comp,
+                    char* err, int errlen);
+void vcth_free_image(uint8_t* data);
 void vcth_free(vcth_model* m);
 /* Apply a column-major 4x4 model matrix to every vertex position (host Model::Transform). */
 void vcth_transform(vcth_model* m, const float mat[16]);

@@ -100,6 +100,37 @@
 #define VCT_FIXED_ONE       65536.0f     /* round(x * 2^16) into int64 sums        */
 #define VCT_FIXED_ONE_D     65536.0
 
+/* ---- diffuse maps (albedo = Kd x diffuse map; SURVEY 8a Model::loadMaterials) --
+ * The reference loads a material's map_Kd with stbi_load(path, .., 0), uploads it
+ * as glTexImage2D(GL_RED | GL_RGB | GL_RGBA, GL_UNSIGNED_BYTE) and samples it with
+ * GL_REPEAT wrap and GL_LINEAR magnification (model.cpp:150-226, :212-216) at the
+ * assimp-flipped UV (aiProcess_FlipUVs, model.cpp:24: v' = 1 - v).
+ *  Texture: W x H RGBA8, row 0 = the image's first (top) row = GL's t = 0 row;
+ *    1 / 3 channels expand as GL_RED / GL_RGB sample: (r,0,0,255) / (r,g,b,255).
+ *    (2 channels: the reference leaves `format` uninitialised, model.cpp:200-206;
+ *    such a map is refused and the material keeps Kd.)
+ *  Texel value c / 255.0f per channel (float division).
+ *  T(u, v) for the TexCoords (u, v') of the vertex record (already flipped):
+ *    fu = u - floorf(u), fv = v' - floorf(v')          (non-finite coordinate -> 0)
+ *    s = fu * W - 0.5,  t = fv * H - 0.5               (texel-centre convention)
+ *    x0 = floorf(s), ax = s - x0, x1 = x0 + 1 (likewise y0, ay, y1), wrapped into
+ *    [0, W) / [0, H) (GL_REPEAT; x0 >= -1 and x1 <= W by construction)
+ *    lerp(a, b, f) = fmaf(f, b - a, a)
+ *    T = lerp(lerp(T[y0][x0], T[y0][x1], ax), lerp(T[y1][x0], T[y1][x1], ax), ay)
+ *    rgb only.  Base level only: voxelization and the G-buffer have no screen-space
+ *    derivative to pick a GL_LINEAR_MIPMAP_LINEAR level from.
+ *  UV of a (triangle, voxel) hit in K1: the voxel centre c projected onto the
+ *    triangle's plane, in voxel units (q0, q1, q2 = the vertices):
+ *      e1 = q1 - q0, e2 = q2 - q0, w = c - q0, dot = (x*x' + y*y') + z*z'
+ *      d11 = e1.e1, d12 = e1.e2, d22 = e2.e2, w1 = w.e1, w2 = w.e2
+ *      den = d11*d22 - d12*d12; b1 = b2 = 0 unless den > 0, else
+ *      b1 = (d22*w1 - d12*w2) / den, b2 = (d11*w2 - d12*w1) / den
+ *      b1 = fmaxf(b1, 0), b2 = fmaxf(b2, 0); if (b1 + b2 > 1) b1 /= s, b2 /= s (s = b1 + b2)
+ *    and in the G-buffer: (b1, b2) = the Moller-Trumbore (u, v) of the nearest hit.
+ *    uv = fmaf(b2, uv2 - uv0, fmaf(b1, uv1 - uv0, uv0)) per component.
+ *  Albedo = Kd.rgb * T.rgb, then (K1) round(albedo * 2^16) into the int64 sums. */
+#define VCT_TEX_MAX_DIM     16384u       /* largest texture edge accepted           */
+
 /* ---- multi-GPU screen tiling ---------------------------------- */
 #define VCT_TILE            64           /* 64x64-pixel tiles, round-robin by rank */
 

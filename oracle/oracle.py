@@ -23,6 +23,21 @@ def build():
     subprocess.run(["make", "-C", HERE, "-s"], check=True)
 
 
+class _Texture(C.Structure):
+    _fields_ = [("rgba8", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32)]
+
+
+def _tex_array(textures):
+    """list of (H, W, 4) uint8 arrays -> (ctypes array of vo_texture, keep-alive list)"""
+    keep = [np.ascontiguousarray(t, np.uint8) for t in textures]
+    arr = (_Texture * max(len(keep), 1))()
+    for i, t in enumerate(keep):
+        assert t.ndim == 3 and t.shape[2] == 4, t.shape
+        arr[i].rgba8 = t.ctypes.data_as(C.c_void_p)
+        arr[i].height, arr[i].width = t.shape[0], t.shape[1]
+    return arr, keep
+
+
 class _TraceParams(C.Structure):
     _fields_ = [("n", C.c_uint32), ("g0", C.c_float * 3), ("extent", C.c_float), ("aniso", C.c_int),
                 ("n_diffuse", C.c_uint32), ("specular", C.c_uint32), ("eye", C.c_float * 3)]
@@ -45,6 +60,15 @@ def lib():
         L.vo_voxelize.restype = C.c_int
         L.vo_voxelize.argtypes = [C.c_uint32, P, C.c_float, P, C.c_uint32, C.c_uint32, P, C.c_uint32,
                                   P, P, C.c_uint32, P, P]
+        L.vo_voxelize_tex.restype = C.c_int
+        L.vo_voxelize_tex.argtypes = [C.c_uint32, P, C.c_float, P, C.c_uint32, C.c_uint32, P, C.c_uint32,
+                                      P, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32, P, P]
+        L.vo_tex_sample.restype = None
+        L.vo_tex_sample.argtypes = [C.POINTER(_Texture), C.c_float, C.c_float, P]
+        L.vo_tri_bary.restype = None
+        L.vo_tri_bary.argtypes = [P, P, P, P, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.vo_tri_uv.restype = None
+        L.vo_tri_uv.argtypes = [P, C.c_float, C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.vo_resolve.restype = None
         L.vo_resolve.argtypes = [C.c_uint32, P, P, P, P]
         L.vo_inject.restype = None
@@ -70,21 +94,47 @@ def log2(x: float) -> float:
     return float(lib().vo_log2(C.c_float(x)))
 
 
-def voxelize(n, aabb_min, extent, verts, idx, tri_mat=None, kd4=None):
-    """-> (sums6 [n^3,6] int64, counts [n^3] uint32)"""
+def voxelize(n, aabb_min, extent, verts, idx, tri_mat=None, kd4=None, mat_map=None, textures=(), uv_offset=24):
+    """-> (sums6 [n^3,6] int64, counts [n^3] uint32).  mat_map (per material: texture
+    index or -1) + textures ((H, W, 4) uint8) select the diffuse-map rule (vo_voxelize_tex)."""
     verts = np.ascontiguousarray(verts, np.float32)
     idx = np.ascontiguousarray(idx, np.uint32).reshape(-1)
     mat = None if tri_mat is None else np.ascontiguousarray(tri_mat, np.uint32)
     kd = None if kd4 is None else np.ascontiguousarray(kd4, np.float32).reshape(-1, 4)
+    mm = None if mat_map is None else np.ascontiguousarray(mat_map, np.int32).reshape(-1)
+    n_mat = kd.shape[0] if kd is not None else (mm.size if mm is not None else 0)
     g0 = np.asarray(aabb_min, np.float32)
     sums = np.zeros((n ** 3, 6), np.int64)
     counts = np.zeros(n ** 3, np.uint32)
-    rc = lib().vo_voxelize(n, _p(g0), C.c_float(extent), _p(verts), verts.shape[1] * 4, verts.shape[0],
-                           _p(idx), idx.size, _p(mat), _p(kd), 0 if kd is None else kd.shape[0],
-                           _p(sums), _p(counts))
+    tarr, keep = _tex_array(textures)
+    rc = lib().vo_voxelize_tex(n, _p(g0), C.c_float(extent), _p(verts), verts.shape[1] * 4, verts.shape[0],
+                               _p(idx), idx.size, _p(mat), _p(kd), n_mat, _p(mm), uv_offset,
+                               C.cast(tarr, C.c_void_p), len(keep), _p(sums), _p(counts))
     if rc != 0:
         raise ValueError("oracle voxelize: index out of range")
     return sums, counts
+
+
+def tex_sample(texture, u, v):
+    """vct_spec.h T(u, v).rgb of one (H, W, 4) uint8 texture -> float32[3]"""
+    tarr, keep = _tex_array([texture])
+    out = np.zeros(3, np.float32)
+    lib().vo_tex_sample(tarr, C.c_float(u), C.c_float(v), _p(out))
+    return out
+
+
+def tri_bary(q0, q1, q2, c):
+    b1, b2 = C.c_float(), C.c_float()
+    f = lambda a: np.ascontiguousarray(a, np.float32)
+    q0, q1, q2, c = f(q0), f(q1), f(q2), f(c)
+    lib().vo_tri_bary(_p(q0), _p(q1), _p(q2), _p(c), C.byref(b1), C.byref(b2))
+    return b1.value, b2.value
+
+
+def tri_uv(uv6, b1, b2):
+    u, v = C.c_float(), C.c_float()
+    lib().vo_tri_uv(_p(np.ascontiguousarray(uv6, np.float32)), C.c_float(b1), C.c_float(b2), C.byref(u), C.byref(v))
+    return u.value, v.value
 
 
 def resolve(n, sums, counts):
@@ -158,9 +208,10 @@ def composite(n, aabb_min, extent, albedo_occ, pos4, nrm4, alb4, diffuse4, spec4
     return lin, rgba
 
 
-def pipeline(n, aabb_min, extent, verts, idx, tri_mat, kd4, light_dir, light_color=(1, 1, 1), aniso=True):
+def pipeline(n, aabb_min, extent, verts, idx, tri_mat, kd4, light_dir, light_color=(1, 1, 1), aniso=True,
+             mat_map=None, textures=()):
     """K1 -> resolve -> K2 -> K3 on the CPU.  -> dict of every intermediate."""
-    sums, counts = voxelize(n, aabb_min, extent, verts, idx, tri_mat, kd4)
+    sums, counts = voxelize(n, aabb_min, extent, verts, idx, tri_mat, kd4, mat_map, textures)
     ao, nm = resolve(n, sums, counts)
     r0 = inject(n, ao, nm, light_dir, light_color)
     pyr = build_mips(n, r0, aniso)

@@ -37,8 +37,11 @@ struct vct_ctx {
     float *albedo_occ, *normal;     /* resolved K1 voxels */
     int64_t* sums;                  /* [n^3][6] */
     uint32_t* counts;
-    float* tri;                     /* [n_tri][4][4]: v0, e1, e2, kd (as the HIP mesh records) */
+    float* tri;                     /* [n_tri][4][4]: v0, e1, e2, (kd, map as int bits) (the HIP mesh records) */
+    float* uv;                      /* [n_tri][6] TexCoords of a textured voxelization, else NULL */
     uint32_t n_tri;
+    vo_texture* tex;                /* vct_set_textures (own copies of the texels) */
+    uint32_t n_tex;
     int voxelized, injected, mipped;
     int comm;               /* vct_comm_init was called (one rank) */
     char err[256];
@@ -70,7 +73,9 @@ const char* vct_last_error(const vct_ctx* c) { return c ? c->err : "null context
 void vct_destroy(vct_ctx* c) {
     if (!c) return;
     free(c->r0); free(c->pyr); free(c->albedo_occ); free(c->normal);
-    free(c->sums); free(c->counts); free(c->tri);
+    free(c->sums); free(c->counts); free(c->tri); free(c->uv);
+    for (uint32_t i = 0; i < c->n_tex; ++i) free((void*)c->tex[i].rgba8);
+    free(c->tex);
     free(c);
 }
 
@@ -129,26 +134,39 @@ vct_status vct_synchronize(vct_ctx* c) { return c ? VCT_OK : VCT_EINVAL; }
 /* ---- K1 ------------------------------------------------------------------- */
 static vct_status voxelize_common(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
                                   const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
-                                  const float* kd4, uint32_t n_mat) {
+                                  const float* kd4, const int32_t* map, uint32_t n_mat, uint32_t uv_offset) {
     if (!c) return VCT_EINVAL;
     if (n_idx % 3 != 0) return fail(c, VCT_EINVAL, "n_idx must be a multiple of 3");
     if (n_idx > 0 && (!verts || !idx)) return fail(c, VCT_EINVAL, "null vertex or index array");
     if (stride < 12 || stride % 4 != 0) return fail(c, VCT_EINVAL, "vertex_stride < 12 or not a multiple of 4");
     if (kd4 && n_mat == 0) return fail(c, VCT_EINVAL, "material_kd4 with n_materials == 0");
+    if (map && n_mat == 0) return fail(c, VCT_EINVAL, "material_map with n_materials == 0");
+    if (map && (uv_offset % 4 != 0 || (uint64_t)uv_offset + 8 > stride))
+        return fail(c, VCT_EINVAL, "uv_offset must be a multiple of 4 with uv_offset + 8 <= vertex_stride");
+    if (map)
+        for (uint32_t i = 0; i < n_mat; ++i)
+            if (map[i] < -1 || (map[i] >= 0 && (uint32_t)map[i] >= c->n_tex))
+                return fail(c, VCT_EINVAL, "material_map entry is not a texture of vct_set_textures or -1");
     const size_t nv = (size_t)c->n * c->n * c->n;
     const uint32_t n_tri = n_idx / 3;
     memset(c->sums, 0, nv * 6 * sizeof(int64_t));
     memset(c->counts, 0, nv * sizeof(uint32_t));
     /* the mesh records the G-buffer caster reads (k1_tri_setup) */
     free(c->tri);
+    free(c->uv);
+    c->uv = NULL;
     c->tri = (float*)calloc((size_t)(n_tri ? n_tri : 1) * 16, sizeof(float));
-    if (!c->tri) return fail(c, VCT_ENOMEM, "mesh records");
+    if (map) c->uv = (float*)calloc((size_t)(n_tri ? n_tri : 1) * 6, sizeof(float));
+    if (!c->tri || (map && !c->uv)) return fail(c, VCT_ENOMEM, "mesh records");
     c->n_tri = n_tri;
     int bad = 0;
     for (uint32_t t = 0; t < n_tri; ++t) {
         const uint32_t vi[3] = {idx[3 * t], idx[3 * t + 1], idx[3 * t + 2]};
         const uint32_t m = tri_mat ? tri_mat[t] : 0u;
-        if (vi[0] >= n_verts || vi[1] >= n_verts || vi[2] >= n_verts || (kd4 && m >= n_mat)) { bad = 1; continue; }
+        if (vi[0] >= n_verts || vi[1] >= n_verts || vi[2] >= n_verts || ((kd4 || map) && m >= n_mat)) {
+            bad = 1;
+            continue;
+        }
         const float* p0 = (const float*)((const char*)verts + (size_t)vi[0] * stride);
         const float* p1 = (const float*)((const char*)verts + (size_t)vi[1] * stride);
         const float* p2 = (const float*)((const char*)verts + (size_t)vi[2] * stride);
@@ -157,27 +175,74 @@ static vct_status voxelize_common(vct_ctx* c, const void* verts, uint32_t stride
         r[4] = p1[0] - p0[0]; r[5] = p1[1] - p0[1]; r[6] = p1[2] - p0[2];
         r[8] = p2[0] - p0[0]; r[9] = p2[1] - p0[1]; r[10] = p2[2] - p0[2];
         r[12] = kd4 ? kd4[4 * m] : 1.0f; r[13] = kd4 ? kd4[4 * m + 1] : 1.0f; r[14] = kd4 ? kd4[4 * m + 2] : 1.0f;
+        const int32_t tex = map ? map[m] : -1;
+        memcpy(r + 15, &tex, 4);
+        if (tex >= 0)
+            for (int k = 0; k < 3; ++k)
+                memcpy(c->uv + (size_t)t * 6 + 2 * k,
+                       (const char*)verts + (size_t)vi[k] * stride + uv_offset, 8);
     }
-    if (n_idx && vo_voxelize(c->n, c->cfg.aabb_min, c->cfg.extent, verts, stride, n_verts, idx, n_idx, tri_mat, kd4,
-                             n_mat, c->sums, c->counts) != 0)
+    if (n_idx && vo_voxelize_tex(c->n, c->cfg.aabb_min, c->cfg.extent, verts, stride, n_verts, idx, n_idx, tri_mat,
+                                 kd4, n_mat, map, uv_offset, c->tex, c->n_tex, c->sums, c->counts) != 0)
         bad = 1;
     vo_resolve(c->n, c->sums, c->counts, c->albedo_occ, c->normal);
     c->voxelized = !bad;     /* a partial grid (bad indices) is refused by inject / mips / trace */
     c->injected = c->mipped = 0;
-    if (bad) return fail(c, VCT_EINVAL, "vertex or material index out of range");
+    if (bad) return fail(c, VCT_EINVAL, "vertex, material or diffuse-map index out of range");
     return VCT_OK;
 }
 
 vct_status vct_voxelize(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts, const uint32_t* idx,
                         uint32_t n_idx, const uint32_t* tri_mat, const float* kd4, uint32_t n_mat) {
-    return voxelize_common(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, n_mat);
+    return voxelize_common(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, NULL, n_mat, 0);
 }
 
 vct_status vct_voxelize_device(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts, const uint32_t* idx,
                                uint32_t n_idx, const uint32_t* tri_mat, const float* kd4, uint32_t n_mat) {
     if (c && ((kd4 && ((uintptr_t)kd4 & 15)) || ((uintptr_t)verts & 3)))
         return fail(c, VCT_EINVAL, "material_kd4 must be 16-byte and verts 4-byte aligned");
-    return voxelize_common(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, n_mat);
+    return voxelize_common(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, NULL, n_mat, 0);
+}
+
+vct_status vct_voxelize_textured(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                                 const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat, const float* kd4,
+                                 const int32_t* map, uint32_t n_mat, uint32_t uv_offset) {
+    return voxelize_common(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, map, n_mat, uv_offset);
+}
+
+vct_status vct_voxelize_textured_device(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                                        const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
+                                        const float* kd4, const int32_t* map, uint32_t n_mat, uint32_t uv_offset) {
+    if (c && ((kd4 && ((uintptr_t)kd4 & 15)) || ((uintptr_t)verts & 3) || ((uintptr_t)map & 3)))
+        return fail(c, VCT_EINVAL, "material_kd4 must be 16-byte, verts and material_map 4-byte aligned");
+    return voxelize_common(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, map, n_mat, uv_offset);
+}
+
+vct_status vct_set_textures(vct_ctx* c, const vct_texture* t, uint32_t n) {
+    if (!c) return VCT_EINVAL;
+    if (n && !t) return fail(c, VCT_EINVAL, "null texture array");
+    for (uint32_t i = 0; i < n; ++i)
+        if (!t[i].rgba8 || t[i].width == 0 || t[i].height == 0 || t[i].width > VCT_TEX_MAX_DIM ||
+            t[i].height > VCT_TEX_MAX_DIM)
+            return fail(c, VCT_EINVAL, "texture: null data or size outside 1..VCT_TEX_MAX_DIM");
+    for (uint32_t i = 0; i < c->n_tex; ++i) free((void*)c->tex[i].rgba8);
+    free(c->tex);
+    c->tex = NULL;
+    c->n_tex = 0;
+    if (!n) return VCT_OK;
+    c->tex = (vo_texture*)calloc(n, sizeof(vo_texture));
+    if (!c->tex) return fail(c, VCT_ENOMEM, "texture table");
+    for (uint32_t i = 0; i < n; ++i) {
+        const size_t bytes = (size_t)t[i].width * t[i].height * 4;
+        uint8_t* copy = (uint8_t*)malloc(bytes);
+        if (!copy) { c->n_tex = i; return fail(c, VCT_ENOMEM, "texture"); }
+        memcpy(copy, t[i].rgba8, bytes);
+        c->tex[i].rgba8 = copy;
+        c->tex[i].width = t[i].width;
+        c->tex[i].height = t[i].height;
+        c->n_tex = i + 1;
+    }
+    return VCT_OK;
 }
 
 /* ---- K2 / K3 ---------------------------------------------------------------- */
@@ -400,6 +465,19 @@ static float ray_tri(const float* r, float px, float py, float pz, float dx, flo
     return dot3(e2[0], e2[1], e2[2], qx, qy, qz) * inv;
 }
 
+/* Moller-Trumbore (u, v) of a ray known to hit the triangle (ray_tri's operations) */
+static void ray_tri_bary(const float* r, float px, float py, float pz, float dx, float dy, float dz, float* u,
+                         float* v) {
+    const float *v0 = r, *e1 = r + 4, *e2 = r + 8;
+    const float pvx = dy * e2[2] - dz * e2[1], pvy = dz * e2[0] - dx * e2[2], pvz = dx * e2[1] - dy * e2[0];
+    const float det = dot3(e1[0], e1[1], e1[2], pvx, pvy, pvz);
+    const float inv = 1.0f / det;
+    const float tx = px - v0[0], ty = py - v0[1], tz = pz - v0[2];
+    *u = dot3(tx, ty, tz, pvx, pvy, pvz) * inv;
+    const float qx = ty * e1[2] - tz * e1[1], qy = tz * e1[0] - tx * e1[2], qz = tx * e1[1] - ty * e1[0];
+    *v = dot3(dx, dy, dz, qx, qy, qz) * inv;
+}
+
 static vct_status gbuffer(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h, float rough, float* pos4,
                           float* nrm4, float* alb4) {
     if (!c || !cam || !pos4 || !nrm4 || !alb4 || w == 0 || h == 0) return VCT_EINVAL;
@@ -440,7 +518,17 @@ static vct_status gbuffer(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_
             pos4[4 * p] = P[0] + dx * best; pos4[4 * p + 1] = P[1] + dy * best; pos4[4 * p + 2] = P[2] + dz * best;
             pos4[4 * p + 3] = 1.0f;
             nrm4[4 * p] = nx; nrm4[4 * p + 1] = ny; nrm4[4 * p + 2] = nz; nrm4[4 * p + 3] = 0.0f;
-            alb4[4 * p] = kd[0]; alb4[4 * p + 1] = kd[1]; alb4[4 * p + 2] = kd[2]; alb4[4 * p + 3] = rough;
+            float ar = kd[0], ag = kd[1], ab = kd[2];
+            int32_t tex;
+            memcpy(&tex, kd + 3, 4);
+            if (c->uv && tex >= 0 && (uint32_t)tex < c->n_tex) {   /* albedo = Kd x T(uv of the hit) */
+                float b1, b2, u, v, rgb[3];
+                ray_tri_bary(c->tri + (size_t)hit * 16, P[0], P[1], P[2], dx, dy, dz, &b1, &b2);
+                vo_tri_uv(c->uv + (size_t)hit * 6, b1, b2, &u, &v);
+                vo_tex_sample(&c->tex[tex], u, v, rgb);
+                ar = kd[0] * rgb[0]; ag = kd[1] * rgb[1]; ab = kd[2] * rgb[2];
+            }
+            alb4[4 * p] = ar; alb4[4 * p + 1] = ag; alb4[4 * p + 2] = ab; alb4[4 * p + 3] = rough;
         }
     return VCT_OK;
 }

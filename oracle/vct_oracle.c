@@ -99,25 +99,84 @@ static void cand_range(float mn, float mx, uint32_t n, int* lo, int* hi) {
     *lo = l; *hi = h;
 }
 
-int vo_voxelize(uint32_t n, const float g0[3], float extent,
-                const void* verts, uint32_t stride, uint32_t n_verts,
-                const uint32_t* idx, uint32_t n_idx,
-                const uint32_t* tri_mat, const float* kd4, uint32_t n_mat,
-                int64_t* sums6, uint32_t* counts) {
+/* --- diffuse maps (vct_spec.h "diffuse maps"; SURVEY 8a Model::loadMaterials,
+ *     model.cpp:150-226: stbi_load -> glTexImage2D, GL_REPEAT / GL_LINEAR :212-216) */
+static float tex_lerp(float a, float b, float f) { return fmaf(f, b - a, a); }
+
+void vo_tex_sample(const vo_texture* t, float u, float v, float rgb[3]) {
+    if (!isfinite(u)) u = 0.0f;
+    if (!isfinite(v)) v = 0.0f;
+    const float fu = u - floorf(u), fv = v - floorf(v);
+    const float s = fu * (float)t->width - 0.5f, tt = fv * (float)t->height - 0.5f;
+    const float sx = floorf(s), sy = floorf(tt);
+    const float ax = s - sx, ay = tt - sy;
+    int x0 = (int)sx, y0 = (int)sy, x1 = x0 + 1, y1 = y0 + 1;
+    const int W = (int)t->width, H = (int)t->height;
+    if (x0 < 0) x0 += W;
+    if (y0 < 0) y0 += H;
+    if (x1 >= W) x1 -= W;
+    if (y1 >= H) y1 -= H;
+    const uint8_t* p00 = t->rgba8 + 4 * ((size_t)y0 * W + x0);
+    const uint8_t* p10 = t->rgba8 + 4 * ((size_t)y0 * W + x1);
+    const uint8_t* p01 = t->rgba8 + 4 * ((size_t)y1 * W + x0);
+    const uint8_t* p11 = t->rgba8 + 4 * ((size_t)y1 * W + x1);
+    for (int c = 0; c < 3; ++c) {
+        const float t00 = (float)p00[c] / 255.0f, t10 = (float)p10[c] / 255.0f;
+        const float t01 = (float)p01[c] / 255.0f, t11 = (float)p11[c] / 255.0f;
+        rgb[c] = tex_lerp(tex_lerp(t00, t10, ax), tex_lerp(t01, t11, ax), ay);
+    }
+}
+
+void vo_tri_bary(const float q0[3], const float q1[3], const float q2[3], const float c[3], float* b1, float* b2) {
+    const v3 e1 = {q1[0] - q0[0], q1[1] - q0[1], q1[2] - q0[2]};
+    const v3 e2 = {q2[0] - q0[0], q2[1] - q0[1], q2[2] - q0[2]};
+    const v3 w = {c[0] - q0[0], c[1] - q0[1], c[2] - q0[2]};
+    const float d11 = v3dot(e1, e1), d12 = v3dot(e1, e2), d22 = v3dot(e2, e2);
+    const float w1 = v3dot(w, e1), w2 = v3dot(w, e2);
+    const float den = d11 * d22 - d12 * d12;
+    float a = 0.0f, b = 0.0f;
+    if (den > 0.0f) {
+        a = (d22 * w1 - d12 * w2) / den;
+        b = (d11 * w2 - d12 * w1) / den;
+    }
+    a = fmaxf(a, 0.0f);
+    b = fmaxf(b, 0.0f);
+    const float s = a + b;
+    if (s > 1.0f) { a = a / s; b = b / s; }
+    *b1 = a;
+    *b2 = b;
+}
+
+void vo_tri_uv(const float uv6[6], float b1, float b2, float* u, float* v) {
+    *u = fmaf(b2, uv6[4] - uv6[0], fmaf(b1, uv6[2] - uv6[0], uv6[0]));
+    *v = fmaf(b2, uv6[5] - uv6[1], fmaf(b1, uv6[3] - uv6[1], uv6[1]));
+}
+
+int vo_voxelize_tex(uint32_t n, const float g0[3], float extent,
+                    const void* verts, uint32_t stride, uint32_t n_verts,
+                    const uint32_t* idx, uint32_t n_idx,
+                    const uint32_t* tri_mat, const float* kd4, uint32_t n_mat,
+                    const int32_t* mat_map, uint32_t uv_offset, const vo_texture* tex, uint32_t n_tex,
+                    int64_t* sums6, uint32_t* counts) {
     const float inv_h = (float)n / extent;
     const uint32_t n_tri = n_idx / 3;
     for (uint32_t t = 0; t < n_tri; ++t) {
         uint32_t vi[3] = {idx[3 * t], idx[3 * t + 1], idx[3 * t + 2]};
         if (vi[0] >= n_verts || vi[1] >= n_verts || vi[2] >= n_verts) return -1;
         uint32_t mat = tri_mat ? tri_mat[t] : 0;
-        if (kd4 && mat >= n_mat) return -1;
+        if ((kd4 || mat_map) && mat >= n_mat) return -1;
+        const int32_t map = mat_map ? mat_map[mat] : -1;
+        if (map < -1 || (map >= 0 && (uint32_t)map >= n_tex)) return -1;
         v3 p[3], q[3];
+        float uv[6] = {0, 0, 0, 0, 0, 0};
         for (int k = 0; k < 3; ++k) {
-            const float* f = (const float*)((const char*)verts + (size_t)vi[k] * stride);
+            const char* rec = (const char*)verts + (size_t)vi[k] * stride;
+            const float* f = (const float*)rec;
             p[k].x = f[0]; p[k].y = f[1]; p[k].z = f[2];
             q[k].x = (p[k].x - g0[0]) * inv_h;
             q[k].y = (p[k].y - g0[1]) * inv_h;
             q[k].z = (p[k].z - g0[2]) * inv_h;
+            if (map >= 0) memcpy(uv + 2 * k, rec + uv_offset, 8);
         }
         /* face normal (world units) and albedo in 16.16 fixed point */
         v3 fn = v3cross(v3sub(p[1], p[0]), v3sub(p[2], p[0]));
@@ -125,13 +184,16 @@ int vo_voxelize(uint32_t n, const float g0[3], float extent,
         if (len > 0.0f) { fn.x = fn.x / len; fn.y = fn.y / len; fn.z = fn.z / len; }
         else { fn.x = 0.0f; fn.y = 0.0f; fn.z = 0.0f; }
         int64_t fix[6];
+        float kd[3];
         for (int c = 0; c < 3; ++c) {
-            float kd = kd4 ? kd4[4 * mat + c] : 1.0f;
-            fix[c] = (int64_t)roundf(kd * VCT_FIXED_ONE);
+            kd[c] = kd4 ? kd4[4 * mat + c] : 1.0f;
+            fix[c] = (int64_t)roundf(kd[c] * VCT_FIXED_ONE);
         }
         fix[3] = (int64_t)roundf(fn.x * VCT_FIXED_ONE);
         fix[4] = (int64_t)roundf(fn.y * VCT_FIXED_ONE);
         fix[5] = (int64_t)roundf(fn.z * VCT_FIXED_ONE);
+        const float q0[3] = {q[0].x, q[0].y, q[0].z}, q1[3] = {q[1].x, q[1].y, q[1].z},
+                    q2[3] = {q[2].x, q[2].y, q[2].z};
 
         int lo[3], hi[3];
         cand_range(fmin3(q[0].x, q[1].x, q[2].x), fmax3(q[0].x, q[1].x, q[2].x), n, &lo[0], &hi[0]);
@@ -143,12 +205,32 @@ int vo_voxelize(uint32_t n, const float g0[3], float extent,
                     v3 c = {(float)x + 0.5f, (float)y + 0.5f, (float)z + 0.5f};
                     if (!tri_box_overlap(q[0], q[1], q[2], c)) continue;
                     size_t v = (size_t)x + (size_t)n * ((size_t)y + (size_t)n * (size_t)z);
-                    for (int k = 0; k < 6; ++k)
+                    int64_t fa[3] = {fix[0], fix[1], fix[2]};
+                    if (map >= 0) {   /* albedo = Kd x T(uv at the voxel centre's projection) */
+                        const float cc[3] = {c.x, c.y, c.z};
+                        float b1, b2, u, w, rgb[3];
+                        vo_tri_bary(q0, q1, q2, cc, &b1, &b2);
+                        vo_tri_uv(uv, b1, b2, &u, &w);
+                        vo_tex_sample(&tex[map], u, w, rgb);
+                        for (int k = 0; k < 3; ++k) fa[k] = (int64_t)roundf((kd[k] * rgb[k]) * VCT_FIXED_ONE);
+                    }
+                    for (int k = 0; k < 3; ++k)
+                        sums6[6 * v + k] = (int64_t)((uint64_t)sums6[6 * v + k] + (uint64_t)fa[k]);
+                    for (int k = 3; k < 6; ++k)
                         sums6[6 * v + k] = (int64_t)((uint64_t)sums6[6 * v + k] + (uint64_t)fix[k]);
                     counts[v] += 1;
                 }
     }
     return 0;
+}
+
+int vo_voxelize(uint32_t n, const float g0[3], float extent,
+                const void* verts, uint32_t stride, uint32_t n_verts,
+                const uint32_t* idx, uint32_t n_idx,
+                const uint32_t* tri_mat, const float* kd4, uint32_t n_mat,
+                int64_t* sums6, uint32_t* counts) {
+    return vo_voxelize_tex(n, g0, extent, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, n_mat, NULL, 0, NULL, 0,
+                           sums6, counts);
 }
 
 void vo_resolve(uint32_t n, const int64_t* sums6, const uint32_t* counts,

@@ -45,6 +45,33 @@ int vo_voxelize(uint32_t n, const float g0[3], float extent,
                 const uint32_t* tri_mat, const float* kd4, uint32_t n_mat,
                 int64_t* sums6, uint32_t* counts);
 
+/* Diffuse maps (include/vct_spec.h "diffuse maps"): RGBA8, row 0 = the image's top row. */
+typedef struct vo_texture {
+    const uint8_t* rgba8;
+    uint32_t width, height;
+} vo_texture;
+
+/* T(u, v).rgb: GL_REPEAT, bilinear at the base level, texel centres at +0.5. */
+void vo_tex_sample(const vo_texture* t, float u, float v, float rgb[3]);
+
+/* K1's (b1, b2) of voxel centre c projected onto triangle q0 q1 q2 (voxel units),
+ * clamped into the triangle. */
+void vo_tri_bary(const float q0[3], const float q1[3], const float q2[3], const float c[3], float* b1, float* b2);
+
+/* uv = fmaf(b2, uv2 - uv0, fmaf(b1, uv1 - uv0, uv0)); uv6 = u0 v0 u1 v1 u2 v2 */
+void vo_tri_uv(const float uv6[6], float b1, float b2, float* u, float* v);
+
+/* K1 with diffuse maps: material m's triangles (mat_map[m] >= 0) contribute
+ * albedo = Kd x T(uv at the voxel centre's projection) per covered voxel; UVs are
+ * the two floats at byte uv_offset of each vertex record.  mat_map NULL = vo_voxelize.
+ * Returns -1 on a bad vertex / material / texture index. */
+int vo_voxelize_tex(uint32_t n, const float g0[3], float extent,
+                    const void* verts, uint32_t stride, uint32_t n_verts,
+                    const uint32_t* idx, uint32_t n_idx,
+                    const uint32_t* tri_mat, const float* kd4, uint32_t n_mat,
+                    const int32_t* mat_map, uint32_t uv_offset, const vo_texture* tex, uint32_t n_tex,
+                    int64_t* sums6, uint32_t* counts);
+
 /* K1 resolve: albedo/occupancy and normal grids from the sums. */
 void vo_resolve(uint32_t n, const int64_t* sums6, const uint32_t* counts,
                 float* albedo_occ4, float* normal4);

@@ -280,6 +280,53 @@ def random_obj(seed=11, nverts=60, nfaces=220):
     return "\n".join(lines) + "\n"
 
 
+# diffuse maps (map_Kd) with texture options and spaces in names: the material's
+# texture path as assimp reports it (aiGetMaterialTexture, aiTextureType_DIFFUSE --
+# what Model::loadMaterialTextures reads, model.cpp:150-158)
+MAPS_MTL = """newmtl plain
+Kd 0.5 0.5 0.5
+map_Kd plain.png
+newmtl clamped
+Kd 0.25 0.5 1
+map_Kd -clamp on clamped.png
+newmtl offset
+Kd 1 1 1
+map_Kd -o 0.5 0.25 offset.png
+newmtl spaced
+Kd 0.1 0.2 0.3
+map_Kd sub dir/with space.png
+newmtl twice
+Kd 0.3 0.3 0.3
+map_Kd first.png
+map_Kd second.png
+newmtl bumponly
+Kd 0.7 0.7 0.7
+map_Bump bump.png
+"""
+MAPS_OBJ = """mtllib scene.mtl
+v 0 0 0
+v 1 0 0
+v 1 1 0
+v 0 1 0
+vt 0 0
+vt 2 0
+vt 2 -1
+vt 0 3
+vn 0 0 1
+usemtl plain
+f 1/1/1 2/2/1 3/3/1
+usemtl clamped
+f 1/1/1 3/3/1 4/4/1
+usemtl offset
+f 2/2/1 3/3/1 4/4/1
+usemtl spaced
+f 1/1/1 2/2/1 4/4/1
+usemtl twice
+f 1/4/1 2/3/1 3/2/1
+usemtl bumponly
+f 4/1/1 3/2/1 2/3/1
+"""
+
 CASES = {"cube": CUBE, "poly": POLY, "edge": EDGE, "degen": DEGEN, "sphere": sphere_obj(),
          "random": random_obj()}
 
@@ -321,7 +368,7 @@ def import_with_assimp(lib, path):
         raise RuntimeError(lib.aiGetErrorString())
     s = sc.contents
     out = {"n_meshes": np.int64(s.nm)}
-    names, ka, kd, ks = [], [], [], []
+    names, ka, kd, ks, dif = [], [], [], [], []
     for i in range(s.nmat):
         m = s.mats[i]
         st = AiString()
@@ -331,7 +378,15 @@ def import_with_assimp(lib, path):
             c = Col4(0, 0, 0, 0)
             lib.aiGetMaterialColor(m, key, 0, 0, C.byref(c))
             dst.append((c.r, c.g, c.b, 1.0))   # model.cpp:48-53: vec4(color.rgb, 1.0)
+        # loadMaterialTextures(aMat, aiTextureType_DIFFUSE, ..) (model.cpp:57, :153-158)
+        path = ""
+        if lib.aiGetMaterialTextureCount(m, 1) > 0:
+            st = AiString()
+            lib.aiGetMaterialTexture(m, 1, 0, C.byref(st), None, None, None, None, None, None)
+            path = st.data[:st.length].decode()
+        dif.append(path)
     out["mat_names"] = np.frombuffer("\n".join(names).encode(), np.uint8)
+    out["mat_diffuse"] = np.frombuffer("\n".join(dif).encode(), np.uint8)
     out["mat_ka"], out["mat_kd"], out["mat_ks"] = (np.array(x, np.float32) for x in (ka, kd, ks))
     for i in range(s.nm):
         m = s.meshes[i].contents
@@ -361,8 +416,11 @@ def main():
     lib.aiGetMaterialColor.argtypes = [C.c_void_p, C.c_char_p, C.c_uint, C.c_uint, C.POINTER(Col4)]
     lib.aiGetMaterialString.argtypes = [C.c_void_p, C.c_char_p, C.c_uint, C.c_uint, C.POINTER(AiString)]
     lib.aiGetErrorString.restype = C.c_char_p
+    lib.aiGetMaterialTextureCount.argtypes = [C.c_void_p, C.c_int]
+    lib.aiGetMaterialTextureCount.restype = C.c_uint
+    lib.aiGetMaterialTexture.argtypes = [C.c_void_p, C.c_int, C.c_uint, C.POINTER(AiString)] + [C.c_void_p] * 6
     with tempfile.TemporaryDirectory() as d:
-        cases = [(n, t, MTL) for n, t in CASES.items()]
+        cases = [(n, t, MTL) for n, t in CASES.items()] + [("maps", MAPS_OBJ, MAPS_MTL)]
         if os.path.exists(REF_MTL):
             cases.append(("nanosuit", NANO_OBJ, open(REF_MTL).read()))
         for name, text, mtl in cases:

@@ -1,6 +1,6 @@
 // obj_fuzz_driver.cpp — runs the host OBJ/MTL loader (host/scene.cpp through
 // include/vct_host.h) and the placement helpers over every file named on the
-// command line.  Built with -fsanitize=address,undefined -fno-sanitize-recover=all
+// command line; with --png first, the PNG decoder (host/png.cpp) instead.  Built with -fsanitize=address,undefined -fno-sanitize-recover=all
 // (tests/native/Makefile): any out-of-bounds access, use-after-free, leak or UB
 // aborts the process.  TEST INFRASTRUCTURE (tests/test_sanitizers.py).
 #include <cstdio>
@@ -8,7 +8,37 @@
 
 #include "vct_host.h"
 
+#include <vector>
+
+static int decode_pngs(int argc, char** argv) {
+    int ok = 0, rejected = 0;
+    for (int a = 2; a < argc; ++a) {
+        FILE* f = std::fopen(argv[a], "rb");
+        if (!f) return 8;
+        std::vector<uint8_t> buf;
+        uint8_t chunk[4096];
+        size_t n;
+        while ((n = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + n);
+        std::fclose(f);
+        uint8_t* data = nullptr;
+        uint32_t w = 0, h = 0;
+        int comp = 0;
+        char err[128];
+        if (vcth_decode_png(buf.data(), buf.size(), &data, &w, &h, &comp, err, (int)sizeof err) != 0) {
+            ++rejected;
+            continue;
+        }
+        unsigned acc = 0;   // touch every byte handed out
+        for (size_t i = 0; i < (size_t)w * h * comp; ++i) acc += data[i];
+        vcth_free_image(data);
+        ok += 1 + (int)(acc & 0);
+    }
+    std::printf("decoded %d rejected %d\n", ok, rejected);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::strcmp(argv[1], "--png") == 0) return decode_pngs(argc, argv);
     int loaded = 0, rejected = 0;
     for (int a = 1; a < argc; ++a) {
         vcth_model* m = nullptr;
@@ -40,6 +70,17 @@ int main(int argc, char** argv) {
             float ka[4], kd[4], ks[4];
             if (vcth_material(m, i, &name, ka, kd, ks) != 0 || !name) return 6;
             acc += std::strlen(name);
+            const char* path = nullptr;
+            int32_t tex = -2;
+            if (vcth_material_diffuse_map(m, i, &path, &tex) != 0 || !path || tex < -1 ||
+                tex >= (int32_t)vcth_num_textures(m))
+                return 9;
+        }
+        for (uint32_t i = 0; i < vcth_num_textures(m); ++i) {
+            const uint8_t* px = nullptr;
+            uint32_t w = 0, h = 0;
+            if (vcth_texture(m, i, &px, &w, &h, nullptr) != 0) return 10;
+            for (size_t k = 0; k < (size_t)w * h * 4; ++k) acc += px[k];
         }
         vcth_free(m);
         if (acc < 0) return 7;

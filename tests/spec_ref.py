@@ -122,7 +122,54 @@ def _roundf(x):
     return (np.sign(x) * np.floor(np.abs(x) + 0.5)).astype(np.int64)
 
 
-def voxelize(n, g0, extent, verts, idx, tri_mat=None, kd4=None):
+# ---- diffuse maps (include/vct_spec.h "diffuse maps"), scalar binary32 -----------
+def _lerp(a, b, f):
+    return fmaf(f, f32(b - a), a)
+
+
+def tex_sample(t, u, v):
+    """T(u, v).rgb of an (H, W, 4) uint8 texture: GL_REPEAT, bilinear, texel centres."""
+    H, W = t.shape[:2]
+    u = float(u) if math.isfinite(u) else 0.0
+    v = float(v) if math.isfinite(v) else 0.0
+    fu, fv = f32(u - math.floor(u)), f32(v - math.floor(v))
+    s, tt = f32(f32(fu * W) - 0.5), f32(f32(fv * H) - 0.5)
+    sx, sy = math.floor(s), math.floor(tt)
+    ax, ay = f32(s - sx), f32(tt - sy)
+    x0, y0 = int(sx) % W, int(sy) % H
+    x1, y1 = (int(sx) + 1) % W, (int(sy) + 1) % H
+    px = lambda y, x, c: f32(float(t[y, x, c]) / 255.0)
+    return [_lerp(_lerp(px(y0, x0, c), px(y0, x1, c), ax), _lerp(px(y1, x0, c), px(y1, x1, c), ax), ay)
+            for c in range(3)]
+
+
+def _dot32(a, b):
+    return f32(f32(f32(a[0] * b[0]) + f32(a[1] * b[1])) + f32(a[2] * b[2]))
+
+
+def tri_bary(q0, q1, q2, c):
+    e1 = [f32(q1[k] - q0[k]) for k in range(3)]
+    e2 = [f32(q2[k] - q0[k]) for k in range(3)]
+    w = [f32(c[k] - q0[k]) for k in range(3)]
+    d11, d12, d22 = _dot32(e1, e1), _dot32(e1, e2), _dot32(e2, e2)
+    w1, w2 = _dot32(w, e1), _dot32(w, e2)
+    den = f32(f32(d11 * d22) - f32(d12 * d12))
+    b1 = b2 = 0.0
+    if den > 0:
+        b1 = f32(f32(f32(d22 * w1) - f32(d12 * w2)) / den)
+        b2 = f32(f32(f32(d11 * w2) - f32(d12 * w1)) / den)
+    b1, b2 = max(b1, 0.0), max(b2, 0.0)
+    s = f32(b1 + b2)
+    if s > 1.0:
+        b1, b2 = f32(b1 / s), f32(b2 / s)
+    return b1, b2
+
+
+def tri_uv(uv, b1, b2):
+    return tuple(fmaf(b2, f32(uv[4 + k] - uv[k]), fmaf(b1, f32(uv[2 + k] - uv[k]), uv[k])) for k in range(2))
+
+
+def voxelize(n, g0, extent, verts, idx, tri_mat=None, kd4=None, mat_map=None, textures=(), uv_offset=24):
     g0 = np.asarray(g0, F)
     inv_h = F(n) / F(extent)
     sums = np.zeros((n ** 3, 6), np.int64)
@@ -150,7 +197,20 @@ def voxelize(n, g0, extent, verts, idx, tri_mat=None, kd4=None):
         c = [ar.astype(F) + F(0.5) for ar in (xx, yy, zz)]
         hit = _sat(q, *c)
         v = (xx + n * (yy + n * zz))[hit]
-        np.add.at(sums, v, fix[None, :])
+        tex = -1 if mat_map is None else int(mat_map[m])
+        if tex < 0:
+            np.add.at(sums, v, fix[None, :])
+        else:   # albedo = Kd x T(uv at the voxel centre's projection), per covered voxel
+            uvf = np.asarray(verts, F)[tri, uv_offset // 4: uv_offset // 4 + 2].reshape(-1)
+            uv = [float(x) for x in uvf]
+            qf = [[float(x) for x in q[k]] for k in range(3)]
+            for vx, vy, vz, vi in zip(xx[hit], yy[hit], zz[hit], v):
+                b1, b2 = tri_bary(qf[0], qf[1], qf[2], (vx + 0.5, vy + 0.5, vz + 0.5))
+                tu, tv = tri_uv(uv, b1, b2)
+                rgb = tex_sample(textures[tex], tu, tv)
+                f = [int(_roundf(f32(f32(float(kd[k]) * rgb[k]) * 65536.0))) for k in range(3)]
+                sums[vi, :3] += f
+                sums[vi, 3:] += fix[3:]
         np.add.at(counts, v, 1)
     return sums, counts.astype(np.uint32)
 

@@ -81,6 +81,36 @@ def test_obj_loader_fuzz_under_sanitizers(drivers, tmp_path_factory, obj, mtl, b
     assert out.startswith("loaded")
 
 
+_PNG_CASES = None
+
+
+def _png_cases():
+    global _PNG_CASES
+    if _PNG_CASES is None:
+        import numpy as np
+        g = np.load(os.path.join(REPO, "tests", "golden", "tex_png_cases.npz"))
+        _PNG_CASES = [g["png_" + n].tobytes() for n in g["names"]]
+    return _PNG_CASES
+
+
+@settings(max_examples=int(os.environ.get("VCT_FUZZ_EXAMPLES", "80")), deadline=None,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(case=st.integers(0, 116), edits=st.lists(st.tuples(st.integers(0, 10 ** 6), st.integers(0, 255)), max_size=8),
+       cut=st.one_of(st.none(), st.integers(0, 10 ** 6)))
+def test_png_decoder_fuzz_under_sanitizers(drivers, tmp_path_factory, case, edits, cut):
+    """host/png.cpp (untrusted texture files) on corrupted PNGs: byte edits anywhere
+    (chunk lengths, IHDR fields, filter bytes, compressed data) and truncations."""
+    blob = bytearray(_png_cases()[case % len(_png_cases())])
+    for at, val in edits:
+        blob[at % len(blob)] = val
+    if cut is not None:
+        blob = blob[:cut % (len(blob) + 1)]
+    d = tmp_path_factory.mktemp("png")
+    (d / "x.png").write_bytes(bytes(blob))
+    (d / "y.png").write_bytes(_png_cases()[(case + 1) % len(_png_cases())])
+    assert _run([drivers[0], "--png", str(d / "x.png"), str(d / "y.png")]).startswith("decoded")
+
+
 def test_obj_loader_sanitized_on_golden_files(drivers):
     """Every OBJ the loader parity tests use, under the sanitizers."""
     import glob

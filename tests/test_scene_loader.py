@@ -38,6 +38,7 @@ def host():
     lib.vcth_material.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_float),
                                   C.POINTER(C.c_float), C.POINTER(C.c_float)]
     lib.vcth_free.argtypes = [C.c_void_p]
+    lib.vcth_material_diffuse_map.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_int32)]
     return lib
 
 
@@ -61,7 +62,9 @@ def load(lib, path):
         name = C.c_char_p()
         ka, kd, ks = (C.c_float * 4)(), (C.c_float * 4)(), (C.c_float * 4)()
         assert lib.vcth_material(h, i, C.byref(name), ka, kd, ks) == 0
-        mats.append((name.value.decode(), list(ka), list(kd), list(ks)))
+        path, tex = C.c_char_p(), C.c_int32()
+        assert lib.vcth_material_diffuse_map(h, i, C.byref(path), C.byref(tex)) == 0
+        mats.append((name.value.decode(), list(ka), list(kd), list(ks), path.value.decode()))
     lib.vcth_free(h)
     return meshes, mats
 
@@ -69,7 +72,7 @@ def load(lib, path):
 def test_golden_files_present():
     names = {os.path.basename(p) for p in GOLDEN}
     assert {"obj_cube.npz", "obj_poly.npz", "obj_edge.npz", "obj_degen.npz", "obj_sphere.npz",
-            "obj_random.npz"} <= names
+            "obj_random.npz", "obj_maps.npz"} <= names
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[4:-4] for p in GOLDEN])
@@ -85,6 +88,8 @@ def test_loader_matches_assimp(host, tmp_path, path):
     assert np.array_equal(np.array([m[1] for m in mats], np.float32), g["mat_ka"])
     assert np.array_equal(np.array([m[2] for m in mats], np.float32), g["mat_kd"])
     assert np.array_equal(np.array([m[3] for m in mats], np.float32), g["mat_ks"])
+    # diffuse map path (map_Kd after assimp's texture-option skipping; loadMaterialTextures input)
+    assert [m[4] for m in mats] == g["mat_diffuse"].tobytes().decode().split("\n")
     # mesh split and order
     assert len(meshes) == int(g["n_meshes"])
     for i, (verts, idx, mat) in enumerate(meshes):

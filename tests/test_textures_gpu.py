@@ -1,0 +1,201 @@
+"""Diffuse maps on the GPU (SURVEY 8a Model::loadMaterials: albedo = Kd x diffuse map).
+
+The textures are 64x64 crops of the reference's own diffuse maps
+(assets/model/test/{arm,body,glass,hand,leg}_dif.png, helmet_diff.png, the map_Kd
+entries of nanosuit.mtl:11,24,37,49,62,74), decoded by the reference's stb_image
+and stored in tests/golden/tex_nanosuit.npz by tests/golden/make_tex_golden.py.
+The scene is vct.scenes.showroom(): nanosuit.mtl's six materials (Kd 0.64) on
+procedural geometry with repeating, negative and per-face TexCoords.
+
+Bar: bit-exact.  K1 (sums, counts, voxels), K2 and K3 against the C oracle's
+vo_voxelize_tex (which tests/test_textures.py pins to tests/spec_ref.py); the
+G-buffer albedo against the CPU backend of include/vct.h (the HIP caster restated);
+K4 on the textured grid against the oracle, outputs and per-pixel steps.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from helpers import gpu_pyramid_flat
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _textures():
+    from vct import scenes
+    g = np.load(os.path.join(GOLD, "tex_nanosuit.npz"))
+    names = [p for _, p in scenes.NANOSUIT_MATERIALS]
+    return names, [np.ascontiguousarray(g["crop_" + p]) for p in names]
+
+
+def _textured_ctx(n, lib=None, level=2):
+    from vct import Context, scenes
+    s = scenes.showroom(level)
+    v, i, m, k = s.arrays()
+    names, tex = _textures()
+    mm = s.material_map(names)
+    g0, E = scenes.grid_for_unit_box(n)
+    ctx = Context(n, g0, E, lib=lib)
+    ctx.set_textures(tex)
+    ctx.voxelize(v, i, m, k, material_map=mm)
+    return ctx, s, (v, i, m, k, mm), tex, (g0, E)
+
+
+@pytest.mark.parametrize("n", [32, 64])
+def test_textured_pipeline_bitexact(gpu_ready, oracle_mod, n):
+    from vct import scenes
+    ctx, s, (v, i, m, k, mm), tex, (g0, E) = _textured_ctx(n)
+    ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    ctx.build_mips()
+    ref = oracle_mod.pipeline(n, g0, E, v, i, m, k, scenes.LIGHT_DIR, mat_map=mm, textures=tex)
+    sums, counts = ctx.download_accum()
+    assert np.array_equal(counts, ref["counts"])
+    assert np.array_equal(sums, ref["sums"]), "textured K1 sums differ"
+    ao, nm = ctx.download_voxels()
+    assert np.array_equal(ao, ref["albedo_occ"]) and np.array_equal(nm, ref["normal"])
+    assert np.array_equal(ctx.download_level(0), ref["r0"])
+    assert np.array_equal(gpu_pyramid_flat(ctx), ref["pyr"])
+    # the maps matter: the Kd-only voxelization of the same scene differs in albedo only
+    plain = oracle_mod.voxelize(n, g0, E, v, i, m, k)
+    assert np.array_equal(plain[1], counts) and np.array_equal(plain[0][:, 3:], sums[:, 3:])
+    assert not np.array_equal(plain[0][:, :3], sums[:, :3])
+    ctx.close()
+
+
+def test_textured_voxelize_device_equals_host_form(gpu_ready):
+    import torch
+    ctx, s, (v, i, m, k, mm), tex, (g0, E) = _textured_ctx(32)
+    sums, counts = ctx.download_accum()
+    dev = torch.device("cuda")
+    ctx.voxelize_device(torch.from_numpy(v).to(dev), torch.from_numpy(i.astype(np.int32)).to(dev),
+                        torch.from_numpy(m.astype(np.int32)).to(dev), torch.from_numpy(k).to(dev),
+                        material_map=torch.from_numpy(mm).to(dev))
+    s2, c2 = ctx.download_accum()
+    assert np.array_equal(s2, sums) and np.array_equal(c2, counts)
+    # an out-of-range map entry is refused on the device path too
+    from vct import VctError
+    bad = mm.copy()
+    bad[0] = 17
+    with pytest.raises(VctError, match="EINVAL"):
+        ctx.voxelize_device(torch.from_numpy(v).to(dev), torch.from_numpy(i.astype(np.int32)).to(dev),
+                            torch.from_numpy(m.astype(np.int32)).to(dev), torch.from_numpy(k).to(dev),
+                            material_map=torch.from_numpy(bad).to(dev))
+    ctx.close()
+
+
+@pytest.mark.parametrize("pos,yaw,pitch", [((0.0, 0.0, 3.0), -90.0, 0.0), ((0.5, -0.2, 1.2), -110.0, -15.0),
+                                           ((-0.3, 0.4, 0.9), -70.0, -25.0)])
+def test_textured_gbuffer_equals_cpu_backend(gpu_ready, oracle_mod, pos, yaw, pitch):
+    """G-buffer albedo = Kd x T(uv of the hit): the HIP raster and ray-cast passes equal
+    the CPU backend's caster bit for bit (positions, normals, albedo, roughness)."""
+    import torch
+    from vct import _lib
+    from vct.camera import Camera
+    cpu = _lib.bind(C.CDLL(oracle_mod.CPU_BACKEND))
+    ctx, *_ = _textured_ctx(32)
+    ref_ctx, *_ = _textured_ctx(32, lib=cpu)
+    cam = Camera(position=pos, yaw=yaw, pitch=pitch)
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    for w, h in ((96, 64), (131, 77)):
+        ref = [np.zeros((h, w, 4), np.float32) for _ in range(3)]
+        ref_ctx.gbuffer_raycast_device(cam, w, h, 0.15, *[r.ctypes.data for r in ref])
+        for fn in (ctx.gbuffer_raster_device, ctx.gbuffer_raycast_device):
+            g = [torch.full((h, w, 4), 5.0, device=dev) for _ in range(3)]
+            fn(cam, w, h, 0.15, *g)
+            torch.cuda.synchronize()
+            for a, b in zip(g, ref):
+                assert np.array_equal(a.cpu().numpy(), b), fn.__name__
+        valid = ref[0][..., 3] > 0
+        assert valid.mean() > 0.3
+        # textured pixels are not Kd-constant
+        assert len(np.unique(ref[2][valid][:, :3], axis=0)) > 50
+    ctx.close()
+    ref_ctx.close()
+
+
+def test_textured_trace_bitexact(gpu_ready, oracle_mod):
+    """K4 over the textured grid and G-buffer: outputs and per-pixel steps equal the oracle."""
+    import torch
+    from vct import scenes
+    from vct.camera import Camera
+    n, w, h = 64, 160, 96
+    ctx, s, (v, i, m, k, mm), tex, (g0, E) = _textured_ctx(n)
+    ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    ctx.build_mips()
+    cam = Camera()
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    gb = [torch.empty((h, w, 4), device=dev) for _ in range(3)]
+    ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)
+    torch.cuda.synchronize()
+    pos, nrm, alb = (t.cpu().numpy() for t in gb)
+    got = ctx.trace(pos, nrm, alb, cam.position)
+    ref_grid = oracle_mod.pipeline(n, g0, E, v, i, m, k, scenes.LIGHT_DIR, mat_map=mm, textures=tex)
+    ref = oracle_mod.trace(n, g0, E, ref_grid["r0"], ref_grid["pyr"], pos, nrm, alb, cam.position)
+    assert np.array_equal(got["diffuse"], ref["diffuse"]) and np.array_equal(got["spec"], ref["spec"])
+    assert np.array_equal(got["steps_px"], ref["steps_px"]) and got["cone_steps"] == ref["cone_steps"]
+    # composite (row f3) with the textured albedo: linear output equals the oracle's
+    d, sp = torch.from_numpy(got["diffuse"]).to(dev), torch.from_numpy(got["spec"]).to(dev)
+    lin = torch.empty((h, w, 4), device=dev)
+    ctx.composite_device(*gb, d, sp, w, h, scenes.LIGHT_DIR, out_linear4=lin)
+    torch.cuda.synchronize()
+    l_ref, _ = oracle_mod.composite(n, g0, E, ref_grid["albedo_occ"], pos, nrm, alb, got["diffuse"], got["spec"],
+                                    np.asarray(scenes.LIGHT_DIR, np.float32) / np.linalg.norm(scenes.LIGHT_DIR))
+    assert np.array_equal(lin.cpu().numpy(), l_ref)
+    ctx.close()
+
+
+def test_cpp_host_textured_model(gpu_ready, tmp_path):
+    """The C++ host end to end with diffuse maps: OBJ + MTL (map_Kd) + PNG files -> the
+    loader decodes the maps (host/png.cpp), ConeTraceRenderer uploads them
+    (vct_set_textures) and voxelizes with vct_voxelize_textured.  The same scene
+    without its map_Kd lines renders a different image with the same cone steps."""
+    import importlib.util
+    import re
+    import subprocess
+    from vct import scenes
+    spec = importlib.util.spec_from_file_location("mtg", os.path.join(GOLD, "make_tex_golden.py"))
+    mtg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mtg)
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "voxel-based-global-illumination_amd", "build", "vct_headless")
+    assert os.path.exists(exe)
+    s = scenes.showroom(1)
+    v, i, m, k = s.arrays()
+    names, tex = _textures()
+    for p, t in zip(names, tex):
+        (tmp_path / p).write_bytes(mtg.write_png(t.astype(np.int64), 6, 8))
+    lines = ["mtllib scene.mtl"]
+    for row in v:
+        lines.append("v %.9g %.9g %.9g" % tuple(row[:3]))
+    for row in v:
+        lines.append("vt %.9g %.9g" % (row[6], 1.0 - row[7]))      # the loader applies FlipUVs
+    tri = i.reshape(-1, 3) + 1
+    for mat in range(k.shape[0]):
+        lines.append(f"usemtl m{mat}")
+        for t in np.flatnonzero(m == mat):
+            lines.append("f " + " ".join(f"{a}/{a}" for a in tri[t]))
+    (tmp_path / "scene.obj").write_text("\n".join(lines) + "\n")
+    out = {}
+    for textured in (True, False):
+        mtl = []
+        for mat in range(k.shape[0]):
+            mtl.append(f"newmtl m{mat}\nKd %.9g %.9g %.9g" % tuple(k[mat, :3]))
+            if textured and s.maps[mat]:
+                mtl.append(f"map_Kd {s.maps[mat]}")
+        (tmp_path / "scene.mtl").write_text("\n".join(mtl) + "\n")
+        ppm = str(tmp_path / f"f{int(textured)}.ppm")
+        p = subprocess.run([exe, str(tmp_path / "scene.obj"), "64", "160", "120", "2", ppm, "--model=identity",
+                            "--grid=unit"], capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        assert "Texture failed" not in p.stdout + p.stderr
+        steps = [int(x) for x in re.findall(r"(\d+) cone steps", p.stdout)]
+        assert len(steps) == 2 and steps[0] == steps[1] > 0, p.stdout
+        out[textured] = (steps[0], open(ppm, "rb").read())
+    assert out[True][0] == out[False][0]
+    assert out[True][1] != out[False][1]

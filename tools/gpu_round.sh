@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 STEPS=${STEPS:-10}
 faulted() { grep -qE "HSA_STATUS_ERROR|Memory access fault|APERTURE_VIOLATION|GPU core dump" "$@"; }
-timeout -k 10 ${TEST_TIMEOUT:-600} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if faulted gpurun_out/pytest_gpu.log; then echo "GPU FAULT in tests"; exit 99; fi

@@ -225,6 +225,9 @@ void vct_destroy(vct_ctx* c) {
     if (g.accum) (void)hipFree(g.accum);
     if (c->k1_err) (void)hipFree(c->k1_err);
     if (c->mesh.tri) (void)hipFree(c->mesh.tri);
+    if (c->mesh.uv) (void)hipFree(c->mesh.uv);
+    if (c->tex.texels) (void)hipFree(c->tex.texels);
+    if (c->tex.desc) (void)hipFree(c->tex.desc);
     if (c->step_tab) (void)hipFree(c->step_tab);
     if (c->spec_keys) (void)hipFree(c->spec_keys);
     if (c->spec_rows) (void)hipFree(c->spec_rows);
@@ -273,9 +276,11 @@ static vct_status voxelize_args(vct_ctx* c, const void* verts, uint32_t stride, 
     return use_device(c);
 }
 
-// K1 on device-resident geometry; `derr` (device int) receives the index-range flag
+// K1 on device-resident geometry; `derr` (device int) receives the index-range flag.
+// dmap (device, may be NULL): each material's diffuse map (vct_voxelize_textured).
 static vct_status voxelize_dev(vct_ctx* c, const void* dv, uint32_t stride, uint32_t n_verts, const uint32_t* di,
-                               uint32_t n_tri, const uint32_t* dm, const float4* dk, uint32_t n_mat, int* derr) {
+                               uint32_t n_tri, const uint32_t* dm, const float4* dk, uint32_t n_mat,
+                               const int32_t* dmap, uint32_t uv_offset, int* derr) {
     Mesh& m = c->mesh;
     const size_t tri_bytes = (size_t)(n_tri ? n_tri : 1) * 4 * sizeof(float4);
     if (m.cap < tri_bytes) {
@@ -286,9 +291,19 @@ static vct_status voxelize_dev(vct_ctx* c, const void* dv, uint32_t stride, uint
         VCT_HIP(hipMalloc(&m.tri, tri_bytes), "hipMalloc mesh");
         m.cap = tri_bytes;
     }
+    const size_t uv_bytes = (size_t)(n_tri ? n_tri : 1) * 2 * sizeof(float4);
+    if (dmap && m.uv_cap < uv_bytes) {
+        VCT_HIP(hipStreamSynchronize(c->stream), "sync");
+        if (m.uv) (void)hipFree(m.uv);
+        m.uv = nullptr;
+        m.uv_cap = 0;
+        VCT_HIP(hipMalloc(&m.uv, uv_bytes), "hipMalloc mesh uv");
+        m.uv_cap = uv_bytes;
+    }
     m.n_tri = n_tri;
+    m.textured = dmap != nullptr;
     VCT_HIP(hipMemsetAsync(derr, 0, 4, c->stream), "memset err");
-    VCT_HIP(launch_voxelize(c, dv, stride, n_verts, di, n_tri, dm, dk, n_mat, derr), "voxelize");
+    VCT_HIP(launch_voxelize(c, dv, stride, n_verts, di, n_tri, dm, dk, n_mat, dmap, uv_offset, derr), "voxelize");
     int herr = 0;
     VCT_HIP(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, c->stream), "download err");
     VCT_HIP(hipStreamSynchronize(c->stream), "voxelize sync");
@@ -296,42 +311,126 @@ static vct_status voxelize_dev(vct_ctx* c, const void* dv, uint32_t stride, uint
     c->grid.voxelized = herr == 0;
     c->grid.injected = c->grid.mipped = false;
     ++c->grid_epoch;
-    if (herr) return fail(c, VCT_EINVAL, "vertex or material index out of range");
+    if (herr) return fail(c, VCT_EINVAL, "vertex, material or diffuse-map index out of range");
     return VCT_OK;
 }
 
-vct_status vct_voxelize(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
-                        const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
-                        const float* kd4, uint32_t n_mat) {
+static vct_status map_args(vct_ctx* c, const int32_t* map, uint32_t n_mat, uint32_t stride, uint32_t uv_offset) {
+    if (!map) return VCT_OK;
+    if (n_mat == 0) return fail(c, VCT_EINVAL, "material_map with n_materials == 0");
+    if (uv_offset % 4 != 0 || (uint64_t)uv_offset + 8 > stride)
+        return fail(c, VCT_EINVAL, "uv_offset must be a multiple of 4 with uv_offset + 8 <= vertex_stride");
+    return VCT_OK;
+}
+
+static vct_status voxelize_host(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                                const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat, const float* kd4,
+                                const int32_t* map, uint32_t n_mat, uint32_t uv_offset) {
     vct_status st = voxelize_args(c, verts, stride, n_idx, idx, kd4, n_mat);
     if (st != VCT_OK) return st;
+    if ((st = map_args(c, map, n_mat, stride, uv_offset)) != VCT_OK) return st;
+    if (map)
+        for (uint32_t i = 0; i < n_mat; ++i)
+            if (map[i] < -1 || (map[i] >= 0 && (uint32_t)map[i] >= c->tex.n))
+                return fail(c, VCT_EINVAL, "material_map[" + std::to_string(i) + "] = " + std::to_string(map[i]) +
+                                               " is not a texture of vct_set_textures (" + std::to_string(c->tex.n) +
+                                               " set) or -1");
     const uint32_t n_tri = n_idx / 3;
     // host -> device staging (the reference keeps CPU copies of vertices / indices
     // next to its GL buffers, mesh.h:17-18; this is the same one-time upload)
-    DeviceBuf dv, di, dm, dk, derr;
+    DeviceBuf dv, di, dm, dk, dmap, derr;
     const size_t vbytes = (size_t)stride * n_verts;
     if (vbytes) VCT_HIP(hipMalloc(&dv.p, vbytes), "hipMalloc verts");
     if (n_idx) VCT_HIP(hipMalloc(&di.p, (size_t)n_idx * 4), "hipMalloc idx");
     if (tri_mat && n_tri) VCT_HIP(hipMalloc(&dm.p, (size_t)n_tri * 4), "hipMalloc mat");
     if (kd4) VCT_HIP(hipMalloc(&dk.p, (size_t)n_mat * 16), "hipMalloc kd");
+    if (map) VCT_HIP(hipMalloc(&dmap.p, (size_t)n_mat * 4), "hipMalloc map");
     VCT_HIP(hipMalloc(&derr.p, 4), "hipMalloc err");
     if (vbytes) VCT_HIP(hipMemcpyAsync(dv.p, verts, vbytes, hipMemcpyHostToDevice, c->stream), "upload verts");
     if (n_idx) VCT_HIP(hipMemcpyAsync(di.p, idx, (size_t)n_idx * 4, hipMemcpyHostToDevice, c->stream), "upload idx");
     if (dm.p) VCT_HIP(hipMemcpyAsync(dm.p, tri_mat, (size_t)n_tri * 4, hipMemcpyHostToDevice, c->stream), "upload mat");
     if (dk.p) VCT_HIP(hipMemcpyAsync(dk.p, kd4, (size_t)n_mat * 16, hipMemcpyHostToDevice, c->stream), "upload kd");
+    if (dmap.p) VCT_HIP(hipMemcpyAsync(dmap.p, map, (size_t)n_mat * 4, hipMemcpyHostToDevice, c->stream), "upload map");
     return voxelize_dev(c, dv.p, stride, n_verts, (const uint32_t*)di.p, n_tri, (const uint32_t*)dm.p,
-                        (const float4*)dk.p, n_mat, (int*)derr.p);
+                        (const float4*)dk.p, n_mat, (const int32_t*)dmap.p, uv_offset, (int*)derr.p);
+}
+
+static vct_status voxelize_device(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                                  const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat, const float* kd4,
+                                  const int32_t* map, uint32_t n_mat, uint32_t uv_offset) {
+    vct_status st = voxelize_args(c, verts, stride, n_idx, idx, kd4, n_mat);
+    if (st != VCT_OK) return st;
+    if ((st = map_args(c, map, n_mat, stride, uv_offset)) != VCT_OK) return st;
+    if ((kd4 && ((uintptr_t)kd4 & 15)) || ((uintptr_t)verts & 3) || ((uintptr_t)map & 3))
+        return fail(c, VCT_EINVAL, "material_kd4 must be 16-byte, verts and material_map 4-byte aligned");
+    if (!c->k1_err) VCT_HIP(hipMalloc((void**)&c->k1_err, 4), "hipMalloc err");
+    return voxelize_dev(c, verts, stride, n_verts, idx, n_idx / 3, tri_mat, (const float4*)kd4, n_mat, map, uv_offset,
+                        c->k1_err);
+}
+
+vct_status vct_voxelize(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                        const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
+                        const float* kd4, uint32_t n_mat) {
+    return voxelize_host(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, nullptr, n_mat, 0);
 }
 
 vct_status vct_voxelize_device(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
                                const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
                                const float* kd4, uint32_t n_mat) {
-    vct_status st = voxelize_args(c, verts, stride, n_idx, idx, kd4, n_mat);
+    return voxelize_device(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, nullptr, n_mat, 0);
+}
+
+vct_status vct_voxelize_textured(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                                 const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat, const float* kd4,
+                                 const int32_t* map, uint32_t n_mat, uint32_t uv_offset) {
+    return voxelize_host(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, map, n_mat, uv_offset);
+}
+
+vct_status vct_voxelize_textured_device(vct_ctx* c, const void* verts, uint32_t stride, uint32_t n_verts,
+                                        const uint32_t* idx, uint32_t n_idx, const uint32_t* tri_mat,
+                                        const float* kd4, const int32_t* map, uint32_t n_mat, uint32_t uv_offset) {
+    return voxelize_device(c, verts, stride, n_verts, idx, n_idx, tri_mat, kd4, map, n_mat, uv_offset);
+}
+
+vct_status vct_set_textures(vct_ctx* c, const vct_texture* tex, uint32_t n) {
+    if (!c || (n && !tex)) return c ? fail(c, VCT_EINVAL, "null texture array") : VCT_EINVAL;
+    uint64_t total = 0;
+    std::vector<TexDesc> desc(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!tex[i].rgba8 || tex[i].width == 0 || tex[i].height == 0 || tex[i].width > VCT_TEX_MAX_DIM ||
+            tex[i].height > VCT_TEX_MAX_DIM)
+            return fail(c, VCT_EINVAL, "texture " + std::to_string(i) + ": null data or size outside 1.." +
+                                           std::to_string(VCT_TEX_MAX_DIM));
+        desc[i] = TexDesc{(uint32_t)total, tex[i].width, tex[i].height, 0u};
+        total += (uint64_t)tex[i].width * tex[i].height;
+        if (total > 0xffffffffull) return fail(c, VCT_EINVAL, "textures exceed 2^32 texels");
+    }
+    vct_status st = use_device(c);
     if (st != VCT_OK) return st;
-    if ((kd4 && ((uintptr_t)kd4 & 15)) || ((uintptr_t)verts & 3))
-        return fail(c, VCT_EINVAL, "material_kd4 must be 16-byte and verts 4-byte aligned");
-    if (!c->k1_err) VCT_HIP(hipMalloc((void**)&c->k1_err, 4), "hipMalloc err");
-    return voxelize_dev(c, verts, stride, n_verts, idx, n_idx / 3, tri_mat, (const float4*)kd4, n_mat, c->k1_err);
+    Textures& t = c->tex;
+    VCT_HIP(hipStreamSynchronize(c->stream), "sync");   // the previous set may still be read
+    if (t.texel_cap < total * 4) {
+        if (t.texels) (void)hipFree(t.texels);
+        t.texels = nullptr;
+        t.texel_cap = 0;
+        VCT_HIP(hipMalloc((void**)&t.texels, total * 4), "hipMalloc textures");
+        t.texel_cap = total * 4;
+    }
+    if (t.desc_cap < (size_t)n * sizeof(TexDesc)) {
+        if (t.desc) (void)hipFree(t.desc);
+        t.desc = nullptr;
+        t.desc_cap = 0;
+        VCT_HIP(hipMalloc((void**)&t.desc, (size_t)n * sizeof(TexDesc)), "hipMalloc texture table");
+        t.desc_cap = (size_t)n * sizeof(TexDesc);
+    }
+    t.n = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        VCT_HIP(hipMemcpy(t.texels + desc[i].off, tex[i].rgba8, (size_t)desc[i].w * desc[i].h * 4,
+                          hipMemcpyHostToDevice),
+                "upload texture");
+    if (n) VCT_HIP(hipMemcpy(t.desc, desc.data(), (size_t)n * sizeof(TexDesc), hipMemcpyHostToDevice), "upload table");
+    t.n = n;
+    return VCT_OK;
 }
 
 vct_status vct_inject_directional(vct_ctx* c, const float dir[3], const float color[3]) {

@@ -136,6 +136,72 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
     return (ax * bx + ay * by) + az * bz;
 }
 
+// ---- diffuse maps (vct_spec.h "diffuse maps") ------------------------------
+// Texture t occupies texels [off, off + w*h) of the context's RGBA8 texel array
+// (one packed dword per texel: r | g << 8 | b << 16 | a << 24), rows top first.
+struct TexDesc {
+    uint32_t off, w, h, pad;
+};
+
+__device__ __forceinline__ float tex_lerp(float a, float b, float f) { return fmaf(f, b - a, a); }
+
+// T(u, v).rgb: GL_REPEAT wrap, bilinear at the base level, texel centres at +0.5
+__device__ __forceinline__ void tex_sample(const uint32_t* __restrict__ texels, TexDesc d, float u, float v,
+                                           float& r, float& g, float& b) {
+    if (!__builtin_isfinite(u)) u = 0.0f;
+    if (!__builtin_isfinite(v)) v = 0.0f;
+    const float fu = u - floorf(u), fv = v - floorf(v);
+    const float s = fu * (float)d.w - 0.5f, t = fv * (float)d.h - 0.5f;
+    const float sx = floorf(s), sy = floorf(t);
+    const float ax = s - sx, ay = t - sy;
+    int x0 = (int)sx, y0 = (int)sy;          // in [-1, w - 1] / [-1, h - 1]
+    int x1 = x0 + 1, y1 = y0 + 1;
+    if (x0 < 0) x0 += (int)d.w;
+    if (y0 < 0) y0 += (int)d.h;
+    if (x1 >= (int)d.w) x1 -= (int)d.w;
+    if (y1 >= (int)d.h) y1 -= (int)d.h;
+    const uint32_t* base = texels + d.off;
+    const uint32_t p00 = base[(size_t)y0 * d.w + x0], p10 = base[(size_t)y0 * d.w + x1];
+    const uint32_t p01 = base[(size_t)y1 * d.w + x0], p11 = base[(size_t)y1 * d.w + x1];
+    float out[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float t00 = (float)((p00 >> (8 * c)) & 255u) / 255.0f, t10 = (float)((p10 >> (8 * c)) & 255u) / 255.0f;
+        const float t01 = (float)((p01 >> (8 * c)) & 255u) / 255.0f, t11 = (float)((p11 >> (8 * c)) & 255u) / 255.0f;
+        out[c] = tex_lerp(tex_lerp(t00, t10, ax), tex_lerp(t01, t11, ax), ay);
+    }
+    r = out[0]; g = out[1]; b = out[2];
+}
+
+// K1's (b1, b2): voxel centre (cx, cy, cz) projected onto the plane of q[9], clamped
+// into the triangle (vct_spec.h); q in voxel units
+__device__ __forceinline__ void tri_bary(const float* __restrict__ q, float cx, float cy, float cz, float& b1,
+                                         float& b2) {
+    const float e1x = q[3] - q[0], e1y = q[4] - q[1], e1z = q[5] - q[2];
+    const float e2x = q[6] - q[0], e2y = q[7] - q[1], e2z = q[8] - q[2];
+    const float wx = cx - q[0], wy = cy - q[1], wz = cz - q[2];
+    const float d11 = dot3(e1x, e1y, e1z, e1x, e1y, e1z), d12 = dot3(e1x, e1y, e1z, e2x, e2y, e2z);
+    const float d22 = dot3(e2x, e2y, e2z, e2x, e2y, e2z);
+    const float w1 = dot3(wx, wy, wz, e1x, e1y, e1z), w2 = dot3(wx, wy, wz, e2x, e2y, e2z);
+    const float den = d11 * d22 - d12 * d12;
+    b1 = 0.0f;
+    b2 = 0.0f;
+    if (den > 0.0f) {
+        b1 = (d22 * w1 - d12 * w2) / den;
+        b2 = (d11 * w2 - d12 * w1) / den;
+    }
+    b1 = fmaxf(b1, 0.0f);
+    b2 = fmaxf(b2, 0.0f);
+    const float s = b1 + b2;
+    if (s > 1.0f) { b1 = b1 / s; b2 = b2 / s; }
+}
+
+// uv = fmaf(b2, uv2 - uv0, fmaf(b1, uv1 - uv0, uv0)) per component; uv[6] = u0 v0 u1 v1 u2 v2
+__device__ __forceinline__ void tri_uv(const float* __restrict__ uv, float b1, float b2, float& u, float& v) {
+    u = fmaf(b2, uv[4] - uv[0], fmaf(b1, uv[2] - uv[0], uv[0]));
+    v = fmaf(b2, uv[5] - uv[1], fmaf(b1, uv[3] - uv[1], uv[1]));
+}
+
 // 64-lane wave sum (wave64 on CDNA: 6 butterfly steps)
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll

@@ -43,7 +43,11 @@ __global__ void __launch_bounds__(256) k_untile(const UntileK k) {
 
 // ---- G-buffer ray caster (input producer for synthetic scenes) -----------
 struct RayK {
-    const float4* tri;  // [n][4]: v0, e1, e2, kd
+    const float4* tri;  // [n][4]: v0, e1, e2, (kd, diffuse map as int bits)
+    const float4* uv;   // [n][2] TexCoords of textured triangles (NULL: untextured voxelization)
+    const uint32_t* texels;   // diffuse maps (vct_set_textures)
+    const TexDesc* tdesc;
+    uint32_t n_tex;
     uint32_t n_tri;
     int w, h;
     float px, py, pz;
@@ -70,6 +74,18 @@ __device__ __forceinline__ float ray_tri(float4 v0, float4 e1, float4 e2, float 
     const float v = dot3(dx, dy, dz, qx, qy, qz) * inv;
     if (v < 0.0f || u + v > 1.0f) return -1.0f;
     return dot3(e2.x, e2.y, e2.z, qx, qy, qz) * inv;
+}
+
+// Moller-Trumbore barycentrics (u, v) of a ray known to hit the triangle (ray_tri's operations)
+__device__ __forceinline__ void ray_tri_bary(float4 v0, float4 e1, float4 e2, float px, float py, float pz, float dx,
+                                             float dy, float dz, float& u, float& v) {
+    const float pvx = dy * e2.z - dz * e2.y, pvy = dz * e2.x - dx * e2.z, pvz = dx * e2.y - dy * e2.x;
+    const float det = dot3(e1.x, e1.y, e1.z, pvx, pvy, pvz);
+    const float inv = 1.0f / det;
+    const float tx = px - v0.x, ty = py - v0.y, tz = pz - v0.z;
+    u = dot3(tx, ty, tz, pvx, pvy, pvz) * inv;
+    const float qx = ty * e1.z - tz * e1.y, qy = tz * e1.x - tx * e1.z, qz = tx * e1.y - ty * e1.x;
+    v = dot3(dx, dy, dz, qx, qy, qz) * inv;
 }
 
 // pixel (x, y) -> unit ray direction (row 0 = top; reference camera, r_voxelization.cpp:16-23)
@@ -101,7 +117,18 @@ __device__ __forceinline__ void write_gbuffer(const RayK& k, int x, int y, float
     if (dot3(nx, ny, nz, dx, dy, dz) > 0.0f) { nx = -nx; ny = -ny; nz = -nz; }
     k.pos[p] = make_float4(k.px + dx * best, k.py + dy * best, k.pz + dz * best, 1.0f);
     k.nrm[p] = make_float4(nx, ny, nz, 0.0f);
-    k.alb[p] = make_float4(kd.x, kd.y, kd.z, k.rough);
+    float ar = kd.x, ag = kd.y, ab = kd.z;
+    const int tex = __float_as_int(kd.w);
+    if (k.uv && tex >= 0 && (uint32_t)tex < k.n_tex) {   // albedo = Kd x T(uv of the hit)
+        float b1, b2, u, v, tr, tg, tb;
+        ray_tri_bary(k.tri[(size_t)hit * 4], e1, e2, k.px, k.py, k.pz, dx, dy, dz, b1, b2);
+        const float4 a = k.uv[(size_t)hit * 2], b = k.uv[(size_t)hit * 2 + 1];
+        const float uv[6] = {a.x, a.y, a.z, a.w, b.x, b.y};
+        tri_uv(uv, b1, b2, u, v);
+        tex_sample(k.texels, k.tdesc[tex], u, v, tr, tg, tb);
+        ar = kd.x * tr; ag = kd.y * tg; ab = kd.z * tb;
+    }
+    k.alb[p] = make_float4(ar, ag, ab, k.rough);
 }
 
 __global__ void __launch_bounds__(256) k_raycast(RayK k) {
@@ -358,6 +385,8 @@ static RayK ray_params(vct_ctx* c, const vct_camera* cam, uint32_t w, uint32_t h
                        float4* nrm, float4* alb) {
     RayK k;
     k.tri = c->mesh.tri; k.n_tri = c->mesh.n_tri;
+    k.uv = c->mesh.textured ? c->mesh.uv : nullptr;
+    k.texels = c->tex.texels; k.tdesc = c->tex.desc; k.n_tex = c->tex.n;
     k.w = (int)w; k.h = (int)h;
     k.px = cam->position[0]; k.py = cam->position[1]; k.pz = cam->position[2];
     k.fx = cam->front[0]; k.fy = cam->front[1]; k.fz = cam->front[2];

@@ -35,9 +35,19 @@ struct Grid {
 };
 
 struct Mesh {
-    float4* tri = nullptr;        // [n_tri][4] : v0, e1 = v1-v0, e2 = v2-v0, (kd rgb, 0)
+    float4* tri = nullptr;        // [n_tri][4] : v0, e1 = v1-v0, e2 = v2-v0, (kd rgb, diffuse map as int bits; -1 none)
+    float4* uv = nullptr;         // [n_tri][2] : (u0 v0 u1 v1), (u2 v2 0 0)  (textured voxelizations)
     uint32_t n_tri = 0;
-    size_t cap = 0;
+    size_t cap = 0, uv_cap = 0;
+    bool textured = false;        // the last voxelization had mapped materials (uv is valid)
+};
+
+// diffuse maps of vct_set_textures (vct_spec.h "diffuse maps")
+struct Textures {
+    uint32_t* texels = nullptr;   // every texture's RGBA8 texels, back to back
+    TexDesc* desc = nullptr;      // [n] offset / size
+    uint32_t n = 0;
+    size_t texel_cap = 0, desc_cap = 0;
 };
 
 struct Scratch {
@@ -79,7 +89,8 @@ struct vct_ctx {
     hipStream_t stream = nullptr;
     vct::Grid grid;
     vct::Mesh mesh;
-    vct::Scratch scratch[12];     // reusable scratch (0 trace host staging, 1 voxelize temps,
+    vct::Textures tex;
+    vct::Scratch scratch[12];    // reusable scratch (0 trace host staging, 1 voxelize temps,
                                   // 2-3 G-buffer bins, 4 K2 work list, 5-6 K4 cone-split hand-over,
                                   // 7 K1 candidate bucket table, 8 multi-device tiles / gather,
                                   // 9 multi-device step counters, 10-11 ray reorder keys / sort temps)
@@ -102,9 +113,12 @@ struct vct_ctx {
 namespace vct {
 
 // K1
+// d_map (device, n_mat entries, may be NULL): diffuse map of each material in c->tex
+// (-1 none); uv_offset: byte offset of the TexCoords in a vertex record (read when d_map)
 hipError_t launch_voxelize(vct_ctx* c, const void* d_verts,
                            uint32_t stride, uint32_t n_verts, const uint32_t* d_idx, uint32_t n_tri,
-                           const uint32_t* d_mat, const float4* d_kd, uint32_t n_mat, int* d_err);
+                           const uint32_t* d_mat, const float4* d_kd, uint32_t n_mat, const int32_t* d_map,
+                           uint32_t uv_offset, int* d_err);
 // K2
 hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb);
 // K3

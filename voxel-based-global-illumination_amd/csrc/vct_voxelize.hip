@@ -32,7 +32,13 @@ struct TriGeom {      // 64 B
 };
 struct TriFix {       // 64 B
     long long fix[6]; // albedo rgb, face normal xyz in 16.16 fixed point
-    long long pad[2];
+    long long tex;    // diffuse map of the triangle's material (-1: albedo = Kd, fix[0..2])
+    long long pad;
+};
+struct TriUV {        // 48 B, textured triangles only
+    float uv[6];      // TexCoords of the three vertices
+    float kd[3];      // material Kd (albedo = Kd x T(uv) per hit)
+    uint32_t pad[3];
 };
 
 __device__ __forceinline__ float fmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
@@ -48,16 +54,21 @@ __device__ __forceinline__ void cand_range(float mn, float mx, int n, int& lo, i
 __global__ void __launch_bounds__(256) k1_tri_setup(
     const char* __restrict__ verts, uint32_t stride, uint32_t n_verts,
     const uint32_t* __restrict__ idx, uint32_t n_tri, const uint32_t* __restrict__ mat,
-    const float4* __restrict__ kd, uint32_t n_mat, int n, float g0x, float g0y, float g0z,
-    float inv_h, TriGeom* __restrict__ geom, TriFix* __restrict__ fixo,
-    unsigned long long* __restrict__ counts, float4* __restrict__ mesh_tri, int* __restrict__ err) {
+    const float4* __restrict__ kd, uint32_t n_mat, const int32_t* __restrict__ map, uint32_t uv_offset,
+    uint32_t n_tex, int n, float g0x, float g0y, float g0z,
+    float inv_h, TriGeom* __restrict__ geom, TriFix* __restrict__ fixo, TriUV* __restrict__ tuv,
+    unsigned long long* __restrict__ counts, float4* __restrict__ mesh_tri, float4* __restrict__ mesh_uv,
+    int* __restrict__ err) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tri) return;
     uint32_t vi[3] = {idx[3 * t], idx[3 * t + 1], idx[3 * t + 2]};
     uint32_t m = mat ? mat[t] : 0u;
     TriGeom g;
     TriFix f;
-    if (vi[0] >= n_verts || vi[1] >= n_verts || vi[2] >= n_verts || (kd && m >= n_mat)) {
+    // the material's diffuse map (material_map, vct_voxelize_textured); out of range -> error
+    const int32_t tex = (map && m < n_mat) ? map[m] : -1;
+    if (vi[0] >= n_verts || vi[1] >= n_verts || vi[2] >= n_verts || (kd && m >= n_mat) || (map && m >= n_mat) ||
+        tex < -1 || (tex >= 0 && (uint32_t)tex >= n_tex)) {
         atomicOr(err, 1);
         g.ext[0] = g.ext[1] = g.ext[2] = 0;
         counts[t] = 0;
@@ -88,7 +99,22 @@ __global__ void __launch_bounds__(256) k1_tri_setup(
     f.fix[3] = (long long)roundf(fn[0] * VCT_FIXED_ONE);
     f.fix[4] = (long long)roundf(fn[1] * VCT_FIXED_ONE);
     f.fix[5] = (long long)roundf(fn[2] * VCT_FIXED_ONE);
-    f.pad[0] = f.pad[1] = 0;
+    f.tex = tex;
+    f.pad = 0;
+    if (tex >= 0) {
+        TriUV r;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float* src = (const float*)(verts + (size_t)vi[k] * stride + uv_offset);
+            r.uv[2 * k] = src[0];
+            r.uv[2 * k + 1] = src[1];
+        }
+        r.kd[0] = alb.x; r.kd[1] = alb.y; r.kd[2] = alb.z;
+        r.pad[0] = r.pad[1] = r.pad[2] = 0;
+        tuv[t] = r;
+        mesh_uv[2 * t + 0] = make_float4(r.uv[0], r.uv[1], r.uv[2], r.uv[3]);
+        mesh_uv[2 * t + 1] = make_float4(r.uv[4], r.uv[5], 0.0f, 0.0f);
+    }
     unsigned long long cnt = 1;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -106,7 +132,7 @@ __global__ void __launch_bounds__(256) k1_tri_setup(
     mesh_tri[4 * t + 0] = make_float4(p[0][0], p[0][1], p[0][2], 0.0f);
     mesh_tri[4 * t + 1] = make_float4(e1[0], e1[1], e1[2], 0.0f);
     mesh_tri[4 * t + 2] = make_float4(e2[0], e2[1], e2[2], 0.0f);
-    mesh_tri[4 * t + 3] = make_float4(alb.x, alb.y, alb.z, 0.0f);
+    mesh_tri[4 * t + 3] = make_float4(alb.x, alb.y, alb.z, __int_as_float(tex));
 }
 
 // ---- exclusive scan of per-triangle candidate counts (u64) ----------------
@@ -239,7 +265,10 @@ __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__
                                                      uint32_t n_tri, const unsigned long long* __restrict__ total_p,
                                                      int n, long long* __restrict__ accum,
                                                      unsigned long long* __restrict__ occ_bits,
-                                                     const uint32_t* __restrict__ starts) {
+                                                     const uint32_t* __restrict__ starts,
+                                                     const TriUV* __restrict__ tuv,
+                                                     const uint32_t* __restrict__ texels,
+                                                     const TexDesc* __restrict__ tdesc) {
     const unsigned long long total = *total_p;
     const unsigned long long c0 = ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x) * kCandPerThread;
     if (c0 >= total) return;
@@ -273,8 +302,21 @@ __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__
         size_t v = (size_t)vx + (size_t)n * ((size_t)vy + (size_t)n * (size_t)vz);
         unsigned long long* a = (unsigned long long*)(accum + 8 * v);
         const TriFix& f = fixr[t];
+        long long fa[3] = {f.fix[0], f.fix[1], f.fix[2]};
+        if (f.tex >= 0) {   // albedo = Kd x T(uv at the voxel centre's projection), per hit
+            const TriUV r = tuv[t];
+            float b1, b2, u, w, tr, tg, tb;
+            tri_bary(q, (float)vx + 0.5f, (float)vy + 0.5f, (float)vz + 0.5f, b1, b2);
+            tri_uv(r.uv, b1, b2, u, w);
+            tex_sample(texels, tdesc[f.tex], u, w, tr, tg, tb);
+            fa[0] = (long long)roundf((r.kd[0] * tr) * VCT_FIXED_ONE);
+            fa[1] = (long long)roundf((r.kd[1] * tg) * VCT_FIXED_ONE);
+            fa[2] = (long long)roundf((r.kd[2] * tb) * VCT_FIXED_ONE);
+        }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) atomicAdd(a + i, (unsigned long long)f.fix[i]);
+        for (int i = 0; i < 3; ++i) atomicAdd(a + i, (unsigned long long)fa[i]);
+#pragma unroll
+        for (int i = 3; i < 6; ++i) atomicAdd(a + i, (unsigned long long)f.fix[i]);
         if (atomicAdd(a + 6, 1ull) == 0ull) atomicOr(occ_bits + (v >> 6), 1ull << (v & 63));   // first hit
     }
 }
@@ -585,12 +627,13 @@ __global__ void __launch_bounds__(256) k2_inject(const float4* __restrict__ albe
 
 hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
                            uint32_t n_verts, const uint32_t* d_idx, uint32_t n_tri, const uint32_t* d_mat,
-                           const float4* d_kd, uint32_t n_mat, int* d_err) {
+                           const float4* d_kd, uint32_t n_mat, const int32_t* d_map, uint32_t uv_offset,
+                           int* d_err) {
     Grid& g = c->grid;
     hipStream_t s = c->stream;
     const size_t nv = (size_t)g.n * g.n * g.n;
     hipError_t e;
-    // scratch layout: geom | fix | counts | offsets | tile sums | total
+    // scratch layout: geom | fix | counts | offsets | tile sums | total | textured triangles' UVs
     const uint32_t n_tiles = (n_tri + kScanTile - 1) / kScanTile;
     size_t off_geom = 0;
     size_t off_fix = off_geom + sizeof(TriGeom) * (size_t)n_tri;
@@ -598,7 +641,8 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
     size_t off_offs = off_cnt + 8 * (size_t)n_tri;
     size_t off_tiles = off_offs + 8 * (size_t)n_tri;
     size_t off_total = off_tiles + 8 * (size_t)(n_tiles + 1);
-    size_t bytes = off_total + 64;           // the bucket table follows (sized once the total is known)
+    size_t off_uv = (off_total + 64 + 255) & ~(size_t)255;
+    size_t bytes = off_uv + (d_map ? sizeof(TriUV) * (size_t)n_tri : 0);   // (the bucket table: scratch 7)
     void* sp;
     if ((e = scratch_get(c, 1, bytes, &sp)) != hipSuccess) return e;
     char* base = (char*)sp;
@@ -608,6 +652,7 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
     unsigned long long* offs = (unsigned long long*)(base + off_offs);
     unsigned long long* tiles = (unsigned long long*)(base + off_tiles);
     unsigned long long* total = (unsigned long long*)(base + off_total);
+    TriUV* tuv = d_map ? (TriUV*)(base + off_uv) : nullptr;
 
     // sparse reset of the previous voxelization (its occupied list), then the bits
     const size_t nwords = nv / 64;
@@ -619,9 +664,9 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
     if ((e = hipMemsetAsync(total, 0, 8, s)) != hipSuccess) return e;
     if (n_tri > 0) {
         hipLaunchKernelGGL(k1_tri_setup, dim3((n_tri + 255) / 256), dim3(256), 0, s,
-                           (const char*)d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat,
-                           (int)g.n, g.g0[0], g.g0[1], g.g0[2], g.inv_h, geom, fix, cnt,
-                           c->mesh.tri, d_err);
+                           (const char*)d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat, d_map,
+                           uv_offset, c->tex.n, (int)g.n, g.g0[0], g.g0[1], g.g0[2], g.inv_h, geom, fix, tuv, cnt,
+                           c->mesh.tri, c->mesh.uv, d_err);
         hipLaunchKernelGGL(k_scan_tiles, dim3(n_tiles), dim3(kScanBlock), 0, s, cnt, offs, tiles, n_tri);
         hipLaunchKernelGGL(k_scan_carry, dim3(1), dim3(kScanBlock), 0, s, tiles, n_tiles, total);
         hipLaunchKernelGGL(k_scan_add, dim3(n_tiles), dim3(kScanBlock), 0, s, offs, tiles, n_tri);
@@ -641,7 +686,8 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
             hipLaunchKernelGGL(k1_bucket_starts, dim3((n_tri + 255) / 256), dim3(256), 0, s, offs, n_tri, total,
                                starts);
             hipLaunchKernelGGL(k1_candidates, dim3((uint32_t)blocks), dim3(256), 0, s, geom, fix, offs,
-                               n_tri, total, (int)g.n, g.accum, g.occ_bits, starts);
+                               n_tri, total, (int)g.n, g.accum, g.occ_bits, starts, tuv, c->tex.texels,
+                               c->tex.desc);
         }
     }
     // the occupied list (kept for the next reset and for K2), then resolve it

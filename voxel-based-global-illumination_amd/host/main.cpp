@@ -55,6 +55,9 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "ERROR::OBJ:: %s\n", err.c_str());   // model.cpp:25-29
         return 1;
     }
+    for (const std::string& e : model->texture_errors)            // model.cpp:219-223
+        std::printf("Texture failed to load at path: %s\n", e.c_str());
+    std::printf("%zu diffuse maps\n", model->textures.size());
     float lo[3], hi[3];
     Model placed = *model;
     placed.Transform(s.model);

@@ -3,6 +3,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 
@@ -55,8 +56,15 @@ bool ConeTraceRenderer::rebuild_scene() {
     Model placed = *model;              // the draw's model matrix, as the GL pass applies it (test.vert)
     placed.Transform(s_.model);
     placed.Flatten(v, idx, tri_mat, kd4);
-    if (!check(vct_voxelize(ctx_, v.data(), sizeof(Vertex), (uint32_t)v.size(), idx.data(), (uint32_t)idx.size(),
-                            tri_mat.data(), kd4.data(), (uint32_t)(kd4.size() / 4)), "vct_voxelize"))
+    // the diffuse maps (Model::loadMaterialTextures): albedo = Kd x map in K1 and the G-buffer
+    std::vector<vct_texture> tex;
+    for (const Texture& t : model->textures) tex.push_back(vct_texture{t.rgba.data(), t.width, t.height});
+    if (!check(vct_set_textures(ctx_, tex.data(), (uint32_t)tex.size()), "vct_set_textures")) return false;
+    const std::vector<int32_t> map = model->MaterialMap();
+    if (!check(vct_voxelize_textured(ctx_, v.data(), sizeof(Vertex), (uint32_t)v.size(), idx.data(),
+                                     (uint32_t)idx.size(), tri_mat.data(), kd4.data(), map.data(),
+                                     (uint32_t)(kd4.size() / 4), (uint32_t)offsetof(Vertex, TexCoords)),
+               "vct_voxelize_textured"))
         return false;
     if (!check(vct_inject_directional(ctx_, s_.light_dir, s_.light_color), "vct_inject_directional")) return false;
     if (!check(vct_build_mips(ctx_), "vct_build_mips")) return false;

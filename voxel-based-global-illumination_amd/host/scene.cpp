@@ -28,7 +28,10 @@
 //    and tangents/bitangents to cos 45 deg.
 #include "scene.h"
 
+#include "png.h"
+
 #include <algorithm>
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -131,6 +134,8 @@ std::string rest_of_line(std::istringstream& ss) {
     return a == std::string::npos ? std::string() : r.substr(a, b - a + 1);
 }
 
+std::string texture_name(const std::string& rest);
+
 void load_mtl(const std::string& path, std::vector<Material>& mats) {
     std::ifstream f(path);
     if (!f) return;                        // assimp logs and continues without the library
@@ -149,8 +154,45 @@ void load_mtl(const std::string& path, std::vector<Material>& mats) {
         } else if (cur && (tag == "Kd" || tag == "Ka" || tag == "Ks")) {
             std::array<float, 4>& k = tag == "Kd" ? cur->Kd : (tag == "Ka" ? cur->Ka : cur->Ks);
             read_floats(ss, k.data(), 3);
+        } else if (cur && tag == "map_Kd") {
+            // the diffuse map (one per material: a later map_Kd replaces it); leading
+            // texture options (-clamp on, -o u v w, ...) are skipped, the rest of the line
+            // is the file name
+            cur->diffuse_map = texture_name(rest_of_line(ss));
         }
     }
+}
+
+// the file name of a map_* statement, as assimp 3.3's MTL reader takes it: while the
+// next token starts with '-', an option is skipped with a fixed token count (matched
+// as a case-insensitive prefix, in this order): -clamp 2; -blendu -blendv -boost
+// -texres -bm -imfchan -type 2; -mm 3; -o -s -t 4 (option + 3 values); any other 1.
+// The rest of the line (spaces kept) is the name.  Pinned by tests/golden/obj_maps.npz.
+std::string texture_name(const std::string& rest) {
+    static const std::pair<const char*, int> opts[] = {
+        {"-clamp", 2}, {"-blendu", 2}, {"-blendv", 2}, {"-boost", 2}, {"-texres", 2}, {"-bm", 2},
+        {"-imfchan", 2}, {"-type", 2}, {"-mm", 3}, {"-o", 4}, {"-s", 4}, {"-t", 4}};
+    auto skip_ws = [&](size_t p) {
+        while (p < rest.size() && std::isspace((unsigned char)rest[p])) ++p;
+        return p;
+    };
+    auto prefix = [&](size_t p, const char* o) {
+        for (size_t i = 0; o[i]; ++i)
+            if (p + i >= rest.size() || std::tolower((unsigned char)rest[p + i]) != o[i]) return false;
+        return true;
+    };
+    size_t p = skip_ws(0);
+    while (p < rest.size() && rest[p] == '-') {
+        int skip = 1;
+        for (const auto& o : opts)
+            if (prefix(p, o.first)) { skip = o.second; break; }
+        for (int i = 0; i < skip; ++i) {   // past this token and the whitespace after it
+            while (p < rest.size() && !std::isspace((unsigned char)rest[p])) ++p;
+            p = skip_ws(p);
+        }
+    }
+    const size_t e = rest.find_last_not_of(" \t\r");
+    return p >= rest.size() || e == std::string::npos || e < p ? std::string() : rest.substr(p, e - p + 1);
 }
 
 // "v", "v/vt", "v//vn", "v/vt/vn"; 1-based or negative (relative) indices
@@ -352,12 +394,18 @@ void calc_tangents(std::vector<Vertex>& vx, const std::vector<unsigned>& tri) {
 
 }  // namespace
 
-bool Model::LoadObj(const std::string& path, std::string* err) {
+bool Model::LoadObj(const std::string& path, std::string* err, bool load_textures) {
     std::ifstream f(path);
     if (!f) {
         if (err) *err = "cannot open " + path;   // model.cpp:25-29 prints and returns
         return false;
     }
+    {   // model.cpp:30: directory = path.substr(0, path.find_last_of('/'))
+        const size_t s = path.find_last_of('/');
+        directory = s == std::string::npos ? std::string(".") : path.substr(0, s);
+    }
+    textures.clear();
+    texture_errors.clear();
     std::vector<V3> P, N;
     std::vector<std::array<float, 2>> T;
     materials.clear();
@@ -480,7 +528,41 @@ bool Model::LoadObj(const std::string& path, std::string* err) {
             meshes.push_back(std::move(m));
         }
     }
+    if (load_textures) LoadTextures();
     return true;
+}
+
+void Model::LoadTextures() {
+    for (Material& mt : materials) {
+        mt.diffuseMaps.clear();
+        if (mt.diffuse_map.empty()) continue;
+        int found = -1;
+        for (size_t j = 0; j < textures.size(); ++j)
+            if (textures[j].path == mt.diffuse_map) { found = (int)j; break; }   // model.cpp:160-166
+        if (found < 0) {
+            // TextureFromFile (model.cpp:188-226): directory + '/' + path, stbi_load(.., 0)
+            PngImage img;
+            Texture t;
+            std::string e;
+            if (!LoadPng(directory + '/' + mt.diffuse_map, &img, &e) || !ExpandToRgba(img, &t.rgba, &e)) {
+                texture_errors.push_back(mt.diffuse_map + ": " + e);
+                continue;
+            }
+            t.type = "texture_diffuse";
+            t.path = mt.diffuse_map;
+            t.width = img.width;
+            t.height = img.height;
+            textures.push_back(std::move(t));
+            found = (int)textures.size() - 1;
+        }
+        mt.diffuseMaps.push_back(found);
+    }
+}
+
+std::vector<int32_t> Model::MaterialMap() const {
+    std::vector<int32_t> m;
+    for (const Material& mt : materials) m.push_back(mt.diffuseMaps.empty() ? -1 : mt.diffuseMaps[0]);
+    return m;
 }
 
 void Model::Transform(const float m[16]) {

@@ -26,11 +26,20 @@ struct Vertex {                    // 56 bytes, stdafx.h:36-42
 };
 static_assert(sizeof(Vertex) == 56, "reference Vertex layout");
 
-struct Material {                  // material.h:5-18 (texture lists omitted: untextured runs)
+struct Texture {                   // stdafx.h:30-34 (GL id -> the decoded texels the C-ABI uploads)
+    std::string type;              // "texture_diffuse" (model.cpp:58)
+    std::string path;              // as written in the .mtl (the dedup key, model.cpp:160-166)
+    uint32_t width = 0, height = 0;
+    std::vector<uint8_t> rgba;     // RGBA8, row 0 = the image's top row (vct_texture)
+};
+
+struct Material {                  // material.h:5-18
     std::string name;
     std::array<float, 4> Ka{0, 0, 0, 1};
     std::array<float, 4> Kd{1, 1, 1, 1};
     std::array<float, 4> Ks{0, 0, 0, 1};
+    std::string diffuse_map;       // map_Kd of the .mtl ("" = none); the only map the VCT path reads
+    std::vector<int> diffuseMaps;  // indices into Model::textures (loadMaterialTextures, model.cpp:57)
 };
 
 struct Mesh {                      // mesh.h:7-26 CPU copies (vertices, indices, material)
@@ -43,9 +52,18 @@ class Model {                      // model.h:8-42
 public:
     std::vector<Mesh> meshes;
     std::vector<Material> materials;
+    std::vector<Texture> textures;   // model.h `textures`: every map loaded once, by path
+    std::string directory;           // the model file's directory (model.cpp:30)
+    std::vector<std::string> texture_errors;   // maps that failed to load (model.cpp:221 prints them)
 
-    // Wavefront OBJ (+ mtllib).  Returns false and fills `err` on failure.
-    bool LoadObj(const std::string& path, std::string* err);
+    // Wavefront OBJ (+ mtllib).  Returns false and fills `err` on failure.  With
+    // load_textures, each material's diffuse map is decoded from `directory` (PNG).
+    bool LoadObj(const std::string& path, std::string* err, bool load_textures = true);
+
+    // loadMaterialTextures for the diffuse maps (model.cpp:150-186): a path already in
+    // `textures` is shared; a map that fails to decode is reported in texture_errors and
+    // the material keeps Kd alone (the reference would sample an incomplete texture).
+    void LoadTextures();
 
     // Apply a 4x4 column-major model matrix (r_voxelization.cpp:26-29 style):
     // p' = (m0 x + m4 y + m8 z + m12, ...), in that float order.
@@ -57,6 +75,9 @@ public:
     // Flatten to the C-ABI arrays: vertices, indices, per-triangle material, Kd table.
     void Flatten(std::vector<Vertex>& v, std::vector<unsigned>& idx, std::vector<unsigned>& tri_mat,
                  std::vector<float>& kd4) const;
+    // material_map of vct_voxelize_textured: each material's first diffuse map (the one
+    // the reference binds as texture_diffuse1) as an index into `textures`, or -1.
+    std::vector<int32_t> MaterialMap() const;
 };
 
 // The model matrix VoxelizationRenderer::Render draws with:

@@ -1,9 +1,11 @@
 // scene_capi.cpp — include/vct_host.h over vcthost::Model (CPU only).
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
 #include "../../include/vct_host.h"
 #include "camera.h"
+#include "png.h"
 #include "scene.h"
 
 struct vcth_model {
@@ -56,6 +58,58 @@ int vcth_material(const vcth_model* m, uint32_t i, const char** name, float ka[4
     }
     return 0;
 }
+
+int vcth_material_diffuse_map(const vcth_model* m, uint32_t i, const char** path, int32_t* texture) {
+    if (!m || i >= m->m.materials.size()) return -1;
+    const vcthost::Material& mt = m->m.materials[i];
+    if (path) *path = mt.diffuse_map.c_str();
+    if (texture) *texture = mt.diffuseMaps.empty() ? -1 : mt.diffuseMaps[0];
+    return 0;
+}
+
+uint32_t vcth_num_textures(const vcth_model* m) { return m ? (uint32_t)m->m.textures.size() : 0u; }
+
+int vcth_texture(const vcth_model* m, uint32_t i, const uint8_t** rgba8, uint32_t* width, uint32_t* height,
+                 const char** path) {
+    if (!m || i >= m->m.textures.size()) return -1;
+    const vcthost::Texture& t = m->m.textures[i];
+    if (rgba8) *rgba8 = t.rgba.data();
+    if (width) *width = t.width;
+    if (height) *height = t.height;
+    if (path) *path = t.path.c_str();
+    return 0;
+}
+
+uint32_t vcth_num_texture_errors(const vcth_model* m) { return m ? (uint32_t)m->m.texture_errors.size() : 0u; }
+
+const char* vcth_texture_error(const vcth_model* m, uint32_t i) {
+    return (m && i < m->m.texture_errors.size()) ? m->m.texture_errors[i].c_str() : nullptr;
+}
+
+int vcth_decode_png(const uint8_t* file, size_t bytes, uint8_t** data, uint32_t* width, uint32_t* height, int* comp,
+                    char* err, int errlen) {
+    if (!file || !data || !width || !height || !comp) return -1;
+    *data = nullptr;
+    vcthost::PngImage img;
+    std::string e;
+    if (!vcthost::DecodePng(file, bytes, &img, &e)) {
+        if (err && errlen > 0) {
+            std::strncpy(err, e.c_str(), (size_t)errlen - 1);
+            err[errlen - 1] = 0;
+        }
+        return -1;
+    }
+    uint8_t* out = (uint8_t*)std::malloc(img.data.size() ? img.data.size() : 1);
+    if (!out) return -1;
+    std::memcpy(out, img.data.data(), img.data.size());
+    *data = out;
+    *width = img.width;
+    *height = img.height;
+    *comp = img.comp;
+    return 0;
+}
+
+void vcth_free_image(uint8_t* data) { std::free(data); }
 
 void vcth_free(vcth_model* m) { delete m; }
 

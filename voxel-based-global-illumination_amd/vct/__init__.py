@@ -27,13 +27,14 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import VCT_ALL_RANKS, VctCamera, VctCommId, VctConfig, VctTraceArgs
+from ._lib import VCT_ALL_RANKS, VctCamera, VctCommId, VctConfig, VctTexture, VctTraceArgs
 
 __all__ = ["Context", "VctError", "VctConfig", "VctCamera", "tiles_for_rank", "tile_offset", "VERTEX_FLOATS",
            "VCT_ALL_RANKS"]
 
 VERTEX_FLOATS = 14          # reference Vertex: Position, Normal, TexCoords, Tangent, Bitangent
 VERTEX_STRIDE = VERTEX_FLOATS * 4
+UV_OFFSET = 24              # offsetof(Vertex, TexCoords) (stdafx.h:36-42, mesh.cpp:49)
 
 
 class VctError(RuntimeError):
@@ -165,14 +166,30 @@ class Context:
         return nl.value, nf.value
 
     # -- K1 / K2 / K3 -----------------------------------------------------
+    def set_textures(self, textures):
+        """Diffuse maps (vct_set_textures): a list of (H, W, 4) uint8 RGBA arrays, row 0 =
+        the image's top row (stbi_load order); [] clears the set."""
+        keep = [np.ascontiguousarray(t, dtype=np.uint8) for t in textures]
+        arr = (VctTexture * max(len(keep), 1))()
+        for i, t in enumerate(keep):
+            if t.ndim != 3 or t.shape[2] != 4:
+                raise VctError(_EINVAL, f"set_textures: texture {i} must be [H, W, 4] uint8, got {t.shape}")
+            arr[i].rgba8 = t.ctypes.data_as(C.c_void_p)
+            arr[i].height, arr[i].width = t.shape[0], t.shape[1]
+        self._check(self.lib.vct_set_textures(self.h, C.cast(arr, C.c_void_p), len(keep)), "set_textures")
+
     def voxelize(self, verts: np.ndarray, idx: np.ndarray, tri_material: np.ndarray | None = None,
-                 kd4: np.ndarray | None = None):
+                 kd4: np.ndarray | None = None, material_map: np.ndarray | None = None,
+                 uv_offset: int = UV_OFFSET):
+        """K1 (vct_voxelize).  With material_map (per material: set_textures index or -1)
+        it is vct_voxelize_textured: albedo = Kd x diffuse map at the hit's TexCoords."""
         verts = np.ascontiguousarray(verts, dtype=np.float32)
         assert verts.ndim == 2 and verts.shape[1] >= 3
         stride = verts.shape[1] * 4
         idx = np.ascontiguousarray(idx, dtype=np.uint32).reshape(-1)
         mat = None if tri_material is None else np.ascontiguousarray(tri_material, dtype=np.uint32).reshape(-1)
         kd = None if kd4 is None else np.ascontiguousarray(kd4, dtype=np.float32)
+        mm = None if material_map is None else np.ascontiguousarray(material_map, dtype=np.int32).reshape(-1)
         if idx.size % 3:
             raise VctError(_EINVAL, f"voxelize: {idx.size} indices, not a multiple of 3")
         if mat is not None and mat.size != idx.size // 3:
@@ -181,16 +198,24 @@ class Context:
         if kd is not None:
             if kd.ndim != 2 or kd.shape[1] != 4:
                 raise VctError(_EINVAL, f"voxelize: kd4 must be [materials, 4], got {kd.shape}")
-        st = self.lib.vct_voxelize(self.h, _fptr(verts), stride, verts.shape[0], _fptr(idx), idx.size,
-                                   _fptr(mat) if mat is not None else None,
-                                   _fptr(kd) if kd is not None else None,
-                                   0 if kd is None else kd.shape[0])
+        n_mat = 0 if kd is None else kd.shape[0]
+        if mm is None:
+            st = self.lib.vct_voxelize(self.h, _fptr(verts), stride, verts.shape[0], _fptr(idx), idx.size,
+                                       _fptr(mat) if mat is not None else None,
+                                       _fptr(kd) if kd is not None else None, n_mat)
+        else:
+            if kd is not None and mm.size != n_mat:
+                raise VctError(_EINVAL, f"voxelize: material_map has {mm.size} entries for {n_mat} materials")
+            st = self.lib.vct_voxelize_textured(self.h, _fptr(verts), stride, verts.shape[0], _fptr(idx), idx.size,
+                                                _fptr(mat) if mat is not None else None,
+                                                _fptr(kd) if kd is not None else None, _fptr(mm), mm.size,
+                                                uv_offset)
         self._check(st, "voxelize")
 
-    def voxelize_device(self, verts, idx, tri_material=None, kd4=None):
+    def voxelize_device(self, verts, idx, tri_material=None, kd4=None, material_map=None, uv_offset=UV_OFFSET):
         """K1 on device-resident torch tensors: verts [V, F] float32 (F >= 3, the
         56-byte Vertex is F = 14), idx [3T] int32/uint32, tri_material [T] int32,
-        kd4 [M, 4] float32."""
+        kd4 [M, 4] float32, material_map [M] int32 (vct_voxelize_textured_device)."""
         if verts.dim() != 2 or verts.shape[1] < 3:
             raise VctError(_EINVAL, f"voxelize_device: verts must be [V, F >= 3], got {tuple(verts.shape)}")
         if str(idx.dtype) in _I64:
@@ -202,10 +227,13 @@ class Context:
         if kd4 is not None and (kd4.dim() != 2 or kd4.shape[1] != 4):
             raise VctError(_EINVAL, f"voxelize_device: kd4 must be [materials, 4], got {tuple(kd4.shape)}")
         nm = 0 if kd4 is None else kd4.shape[0]
-        st = self.lib.vct_voxelize_device(
-            self.h, self._dev(verts, "verts"), verts.shape[1] * 4, verts.shape[0], self._dev(idx, "idx", _I32),
-            n_idx, self._dev(tri_material, "tri_material", _I32, n_idx // 3),
-            self._dev(kd4, "kd4"), nm)
+        args = (self.h, self._dev(verts, "verts"), verts.shape[1] * 4, verts.shape[0], self._dev(idx, "idx", _I32),
+                n_idx, self._dev(tri_material, "tri_material", _I32, n_idx // 3), self._dev(kd4, "kd4"))
+        if material_map is None:
+            st = self.lib.vct_voxelize_device(*args, nm)
+        else:
+            mm = self._dev(material_map, "material_map", ("torch.int32",), max(nm, 1))
+            st = self.lib.vct_voxelize_textured_device(*args, mm, material_map.numel(), uv_offset)
         self._check(st, "voxelize_device")
 
     def inject_directional(self, dir_to_light, color=(1.0, 1.0, 1.0)):

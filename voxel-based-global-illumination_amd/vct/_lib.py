@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("VCT_LIB") or os.path.join(_HERE, "libvct_hip.so")
 EXPORTS = (
     "vct_create", "vct_destroy", "vct_last_error", "vct_status_string", "vct_abi_version",
     "vct_get_config", "vct_set_stream", "vct_synchronize", "vct_create_multi", "vct_num_devices", "vct_trace_form", "vct_voxelize", "vct_voxelize_device",
+    "vct_set_textures", "vct_voxelize_textured", "vct_voxelize_textured_device",
     "vct_inject_directional", "vct_build_mips", "vct_trace", "vct_trace_device",
     "vct_tiles_for_rank", "vct_untile_device", "vct_untile_planes_device", "vct_untile_planes_packed_device",
     "vct_tile_offset", "vct_comm_get_id", "vct_comm_init", "vct_comm_rank", "vct_comm_broadcast_level0",
@@ -51,6 +52,10 @@ class VctCamera(C.Structure):
         ("near_plane", C.c_float),
         ("far_plane", C.c_float),
     ]
+
+
+class VctTexture(C.Structure):
+    _fields_ = [("rgba8", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32)]
 
 
 class VctCommId(C.Structure):
@@ -116,6 +121,9 @@ def bind(lib: C.CDLL) -> C.CDLL:
         "vct_trace_form": (C.c_int32, [P]),
         "vct_voxelize": (i32, [P, P, u32, u32, P, u32, P, P, u32]),
         "vct_voxelize_device": (i32, [P, P, u32, u32, P, u32, P, P, u32]),
+        "vct_set_textures": (i32, [P, P, u32]),
+        "vct_voxelize_textured": (i32, [P, P, u32, u32, P, u32, P, P, P, u32, u32]),
+        "vct_voxelize_textured_device": (i32, [P, P, u32, u32, P, u32, P, P, P, u32, u32]),
         "vct_inject_directional": (i32, [P, C.POINTER(f32), C.POINTER(f32)]),
         "vct_build_mips": (i32, [P]),
         "vct_trace": (i32, [P, P, P, P, u32, u32, C.POINTER(f32), P, P, P, P]),

@@ -13,7 +13,11 @@ and framebuffer sizes:
 * ``courtyard()``: the "San Miguel-class" stand-in (config C5): an open
   courtyard of 1.0 M mostly small triangles (tessellated paving and walls,
   arcades, icosphere tree crowns, tables, hanging foliage);
-* ``random_triangles()``: a triangle soup for voxelization stress / parity.
+* ``random_triangles()``: a triangle soup for voxelization stress / parity;
+* ``showroom()``: a textured scene on the reference's own materials
+  (assets/model/test/nanosuit.mtl: Arm, Body, Glass, Hand, Helmet, Leg, each
+  Kd 0.64 with a map_Kd diffuse map), with TexCoords that repeat (|uv| > 1),
+  go negative and vary per face, for the diffuse-map row (albedo = Kd x map).
 
 Geometry is emitted in the reference ``Vertex`` layout (include/stdafx.h:36-42:
 Position, Normal, TexCoords, Tangent, Bitangent = 14 floats = 56 bytes,
@@ -51,29 +55,40 @@ class Scene:
     idx: list = field(default_factory=list)
     tri_mat: list = field(default_factory=list)
     kd: list = field(default_factory=list)      # rgba rows
+    maps: list = field(default_factory=list)    # per material: diffuse map file name (map_Kd) or None
 
-    def material(self, rgb) -> int:
+    def material(self, rgb, diffuse_map: str | None = None) -> int:
         self.kd.append((float(rgb[0]), float(rgb[1]), float(rgb[2]), 1.0))
+        self.maps.append(diffuse_map)
         return len(self.kd) - 1
 
-    def tri(self, p0, p1, p2, mat: int):
+    def material_map(self, names) -> np.ndarray:
+        """material_map of vct_voxelize_textured for a texture list in `names` order."""
+        return np.array([names.index(m) if m in names else -1 for m in self.maps], np.int32)
+
+    def tri(self, p0, p1, p2, mat: int, uv=None):
+        """uv: three (u, v) TexCoords (stored as given: already in the flipped convention)."""
         p0, p1, p2 = (np.asarray(p, np.float64) for p in (p0, p1, p2))
         n = np.cross(p1 - p0, p2 - p0)
         ln = np.linalg.norm(n)
         n = n / ln if ln > 0 else n
         base = len(self.verts)
-        for p in (p0, p1, p2):
-            self.verts.append([p[0], p[1], p[2], n[0], n[1], n[2]] + [0.0] * (VERTEX_FLOATS - 6))
+        for k, p in enumerate((p0, p1, p2)):
+            t = (0.0, 0.0) if uv is None else (float(uv[k][0]), float(uv[k][1]))
+            self.verts.append([p[0], p[1], p[2], n[0], n[1], n[2], t[0], t[1]] + [0.0] * (VERTEX_FLOATS - 8))
         self.idx += [base, base + 1, base + 2]
         self.tri_mat.append(mat)
 
-    def quad(self, p0, p1, p2, p3, normal, mat: int):
-        """Quad p0..p3 (in order around the edge) whose face normal points along `normal`."""
+    def quad(self, p0, p1, p2, p3, normal, mat: int, uv=None):
+        """Quad p0..p3 (in order around the edge) whose face normal points along `normal`;
+        uv: the four corners' TexCoords."""
         p0, p1, p2, p3 = (np.asarray(p, np.float64) for p in (p0, p1, p2, p3))
+        uv = [(0, 0), (1, 0), (1, 1), (0, 1)] if uv is None else list(uv)
         if np.dot(np.cross(p1 - p0, p2 - p0), normal) < 0:
             p1, p3 = p3, p1
-        self.tri(p0, p1, p2, mat)
-        self.tri(p0, p2, p3, mat)
+            uv = [uv[0], uv[3], uv[2], uv[1]]
+        self.tri(p0, p1, p2, mat, (uv[0], uv[1], uv[2]))
+        self.tri(p0, p2, p3, mat, (uv[0], uv[2], uv[3]))
 
     def box(self, lo, hi, mat: int):
         """Axis-aligned box with outward normals."""
@@ -315,7 +330,53 @@ def courtyard(seed: int = 11) -> Scene:
     return s
 
 
-SCENES = {"cornell": cornell, "atrium": atrium, "courtyard": courtyard}
+# the reference's material library, assets/model/test/nanosuit.mtl:3-77 (name, map_Kd; Kd 0.64)
+NANOSUIT_MATERIALS = (("Arm", "arm_dif.png"), ("Body", "body_dif.png"), ("Glass", "glass_dif.png"),
+                      ("Hand", "hand_dif.png"), ("Helmet", "helmet_diff.png"), ("Leg", "leg_dif.png"))
+NANOSUIT_KD = 0.64
+
+
+def showroom(sphere_level: int = 2) -> Scene:
+    """Textured stand-in on nanosuit.mtl's materials: a floor with tiled UVs (x3,
+    GL_REPEAT), back / side walls with negative and offset UVs, a plinth box per
+    material with per-face [0,1]^2 UVs, and a spherical-UV icosphere (the seam makes
+    some triangles span u in [0.9, 1.1])."""
+    s = Scene("showroom")
+    m = {name: s.material((NANOSUIT_KD,) * 3, path) for name, path in NANOSUIT_MATERIALS}
+    plain = s.material((0.5, 0.45, 0.4))                                     # an unmapped material
+    s.rect_y(-1.0, -1.0, 1.0, -1.0, 1.0, 1, m["Leg"])
+    s.quad((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1), (0, 0, 1), m["Body"],
+           uv=[(0, 0), (3, 0), (3, 3), (0, 3)])                                   # floor-like tiling on the back wall
+    s.quad((-1, -1, -1), (-1, 1, -1), (-1, 1, 1), (-1, -1, 1), (1, 0, 0), m["Arm"],
+           uv=[(-0.5, -0.25), (-0.5, 1.75), (1.5, 1.75), (1.5, -0.25)])          # negative UVs
+    s.quad((1, -1, -1), (1, 1, -1), (1, 1, 1), (1, -1, 1), (-1, 0, 0), plain)
+    for k, name in enumerate(("Hand", "Glass", "Helmet")):
+        x = -0.6 + 0.6 * k
+        lo, hi = np.array([x - 0.2, -1.0, -0.5]), np.array([x + 0.2, -0.55 + 0.15 * k, -0.1])
+        _box_uv(s, lo, hi, m[name])
+    T = _icosphere(sphere_level) * 0.3 + np.array([0.0, 0.2, 0.35])
+    for tri in T:
+        d = (tri - np.array([0.0, 0.2, 0.35])) / 0.3
+        u = 0.5 + np.arctan2(d[:, 2], d[:, 0]) / (2 * np.pi)
+        u = np.where(u - u.min() > 0.5, u - 1.0, u)                           # seam: keep a triangle's u contiguous
+        v = 0.5 - np.arcsin(np.clip(d[:, 1], -1, 1)) / np.pi
+        s.tri(tri[0], tri[1], tri[2], m["Helmet"], uv=list(zip(u, v)))
+    return s
+
+
+def _box_uv(s: Scene, lo, hi, mat):
+    """Axis-aligned box with outward normals and [0,1]^2 TexCoords per face."""
+    x0, y0, z0 = lo
+    x1, y1, z1 = hi
+    s.quad((x0, y0, z0), (x0, y1, z0), (x0, y1, z1), (x0, y0, z1), (-1, 0, 0), mat)
+    s.quad((x1, y0, z0), (x1, y1, z0), (x1, y1, z1), (x1, y0, z1), (1, 0, 0), mat)
+    s.quad((x0, y0, z0), (x1, y0, z0), (x1, y0, z1), (x0, y0, z1), (0, -1, 0), mat)
+    s.quad((x0, y1, z0), (x1, y1, z0), (x1, y1, z1), (x0, y1, z1), (0, 1, 0), mat)
+    s.quad((x0, y0, z0), (x1, y0, z0), (x1, y1, z0), (x0, y1, z0), (0, 0, -1), mat)
+    s.quad((x0, y0, z1), (x1, y0, z1), (x1, y1, z1), (x0, y1, z1), (0, 0, 1), mat)
+
+
+SCENES = {"cornell": cornell, "atrium": atrium, "courtyard": courtyard, "showroom": showroom}
 
 
 # ---------------------------------------------------------------------------
