@@ -88,18 +88,18 @@ typedef struct vct_trace_args {
     uint32_t tile_rank;    /* trace only 64x64 tiles t with t % tile_world == tile_rank     */
     uint32_t tile_world;   /* 0 or 1: every tile                                            */
     uint32_t tile_compact; /* 1: outputs in rank-compact tile layout [local tile][64*64][4] */
-    uint32_t variant;      /* kernel form, 0 = default; all forms give identical results.
-                              low byte: 0 LDS bricks, 1 per-lane gathers, 2 bricks without
-                              the four-face union, 3 row-major lanes; flags: 0x100 no
-                              specular step tables, 0x200 all cones in one workgroup,
-                              0x400 / 0x800 three / two cone parts, 0x1000 four waves
-                              per workgroup, 0x4000 the counting form without counters,
-                              0x8000 ray reordering: pixels traced in the order of the Morton
-                              code of their cone origin's voxel (for incoherent G-buffers such
-                              as G_rand; one-rank full frames only, ignored otherwise);
-                              bits 20-23: diffuse parts of the three-part split (2 default)
-                                                                  */
+    uint32_t variant;      /* 0 = default (every form gives identical results; the context picks
+                              the fastest per workload, see vct_trace_form).  Public overrides:
+                              VCT_VARIANT_FORCE_UNION / _OCCUPANCY (the compiled form),
+                              VCT_VARIANT_REORDER / _SCREEN_ORDER (the ray order of a one-rank
+                              full frame).  Other bits are A/B experiment switches of the
+                              kernel, not part of this interface (csrc/vct_variants.h).      */
 } vct_trace_args;
+
+#define VCT_VARIANT_REORDER        0x8000u     /* trace in the Morton order of the cone origins */
+#define VCT_VARIANT_FORCE_UNION    0x1000000u  /* four-face-union form (4 waves/SIMD)          */
+#define VCT_VARIANT_FORCE_OCCUPANCY 0x2000000u /* occupancy form (5 waves/SIMD)                */
+#define VCT_VARIANT_SCREEN_ORDER   0x4000000u  /* trace in screen order                        */
 
 /* ---- lifetime ---------------------------------------------------------- */
 vct_status  vct_create(const vct_config* cfg, vct_ctx** out);
@@ -198,14 +198,16 @@ vct_status vct_trace(vct_ctx* ctx, const float* gbuf_pos4, const float* gbuf_nrm
 vct_status vct_trace_device(vct_ctx* ctx, const vct_trace_args* args);
 /* The default variant has two bit-identical compiled forms, the four-face-union form
  * (4 waves/SIMD) and the occupancy form (5 waves/SIMD, three-face bricks), and a one-rank
- * full frame can be traced in screen order or with ray reordering (0x8000).  The context
- * times the candidates the variant leaves open on its first counter-free launches of a
- * workload (frame size, tiling, scene, cone set, G-buffer buffer; while timing, each
- * launch waits for the previous timed one) and keeps the fastest, re-timing every 4096
- * launches.  Returns the kept candidate of the current workload -- bit 0 the form
- * (0 union, 1 occupancy), bit 1 ray reordering -- or -1 while it is still being timed.
- * Variant bits 0x1000000 / 0x2000000 force the union / occupancy form, 0x8000 / 0x4000000
- * ray reordering / screen order. */
+ * full frame can be traced in screen order or with ray reordering.  The context keeps a
+ * choice per workload (frame size, tiling, cone set, grid size; up to four workloads,
+ * least recently used replaced): a new workload's first counter-free launches time the
+ * candidates (while timing, each launch waits for the previous timed one), then the
+ * fastest is kept.  Afterwards launches never block: every 16th is timed with events
+ * that are only polled, and the workload is timed again only when its time drifts above
+ * 1.35x the settled time three samples in a row (the scene or the G-buffer changed).
+ * Returns the kept candidate of the last traced workload -- bit 0 the form (0 union,
+ * 1 occupancy), bit 1 ray reordering; a forced candidate when the variant fixes both --
+ * or -1 while it is still being timed. */
 int32_t    vct_trace_form(const vct_ctx* ctx);
 /* Number of 64x64 tiles rank `rank` of `world` traces for a width x height frame. */
 uint32_t   vct_tiles_for_rank(uint32_t width, uint32_t height, uint32_t rank, uint32_t world);
@@ -251,6 +253,29 @@ vct_status vct_comm_broadcast_level0(vct_ctx* ctx, uint32_t root);
 vct_status vct_comm_trace_frame(vct_ctx* ctx, const vct_trace_args* args, int32_t root);
 /* Releases the communicator (vct_destroy also does). */
 vct_status vct_comm_destroy(vct_ctx* ctx);
+/* Failure detection.  The communicator is non-blocking: every vct_comm_*
+ * call waits for its RCCL calls to be issued for at most the context's deadline
+ * (default 300000 ms), polling ncclCommGetAsyncError.  On expiry or an asynchronous
+ * error the communicator is aborted (ncclCommAbort) and the call returns VCT_ECOMM
+ * (vct_comm_init again to continue), so a dead or absent peer ends the frame loop
+ * instead of hanging it. */
+vct_status vct_comm_set_timeout(vct_ctx* ctx, uint32_t timeout_ms);
+/* Waits until the ctx stream's queued work -- collectives included -- has finished,
+ * polling the stream and the communicator with the deadline above. */
+vct_status vct_comm_synchronize(vct_ctx* ctx);
+/* Where a rank's tiles sit in the exchange buffer of vct_comm_trace_frame (and of the
+ * vct.multi driver), in 64x64 tiles: packed for root >= 0 (rank r's [diffuse][spec]
+ * planes of tiles(r) at 2 * vct_tile_offset(r); the root receives every block), padded
+ * for VCT_ALL_RANKS ([nranks][2][max_tiles], one all-gather).  Pure arithmetic. */
+typedef struct vct_comm_layout {
+    uint64_t buffer_tiles;   /* tiles of the whole exchange buffer                   */
+    uint64_t diffuse_tile;   /* first tile of this rank's diffuse plane              */
+    uint64_t spec_tile;      /* first tile of its specular plane                     */
+    uint32_t tiles;          /* tiles the rank traces                                */
+    uint32_t exchange_tiles; /* tiles it contributes to the exchange (both planes)   */
+} vct_comm_layout;
+vct_status vct_comm_frame_layout(uint32_t width, uint32_t height, uint32_t nranks, uint32_t rank, int32_t root,
+                                 vct_comm_layout* out);
 
 /* ---- G-buffer (input producer) -----------------------
  * Ray-casts the triangles of the last vct_voxelize call through `cam` into a

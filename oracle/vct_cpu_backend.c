@@ -447,6 +447,31 @@ vct_status vct_comm_destroy(vct_ctx* c) {
     return VCT_OK;
 }
 
+vct_status vct_comm_set_timeout(vct_ctx* c, uint32_t timeout_ms) {
+    return (c && timeout_ms) ? VCT_OK : VCT_EINVAL;
+}
+
+vct_status vct_comm_synchronize(vct_ctx* c) {
+    if (!c) return VCT_EINVAL;
+    if (!c->comm) return fail(c, VCT_ESTATE, "comm_synchronize before comm_init");
+    return VCT_OK;   /* every call is synchronous here */
+}
+
+vct_status vct_comm_frame_layout(uint32_t w, uint32_t h, uint32_t nranks, uint32_t rank, int32_t root,
+                                 vct_comm_layout* out) {
+    if (!out || nranks == 0 || rank >= nranks || w == 0 || h == 0) return VCT_EINVAL;
+    if (root != VCT_ALL_RANKS && (root < 0 || (uint32_t)root >= nranks)) return VCT_EINVAL;
+    const int all = root == VCT_ALL_RANKS;
+    const uint32_t T = vct_tiles_for_rank(w, h, 0, 1), mine = vct_tiles_for_rank(w, h, rank, nranks);
+    const uint32_t maxt = vct_tiles_for_rank(w, h, 0, nranks);
+    out->buffer_tiles = all ? (uint64_t)nranks * 2 * maxt : (uint64_t)2 * T;
+    out->diffuse_tile = all ? (uint64_t)rank * 2 * maxt : (uint64_t)2 * vct_tile_offset(w, h, rank, nranks);
+    out->spec_tile = out->diffuse_tile + (all ? maxt : mine);
+    out->tiles = mine;
+    out->exchange_tiles = all ? 2 * maxt : 2 * mine;
+    return VCT_OK;
+}
+
 /* ---- G-buffer: the HIP caster restated (csrc/vct_frame.hip) ----------------- */
 static float dot3(float ax, float ay, float az, float bx, float by, float bz) { return (ax * bx + ay * by) + az * bz; }
 

@@ -943,3 +943,65 @@ def test_trace_form_tuner(gpu_ready):
             if ctx.trace_form >= 0:
                 break
         assert ctx.trace_form in (0, 1, 2, 3), "no candidate chosen after 64 launches"
+
+
+@pytest.mark.gpu
+def test_trace_form_tuner_alternating_workloads(gpu_ready):
+    """A host that double-buffers its G-buffer, alternates counting and plain launches and
+    two frame sizes keeps every choice (one tuner entry per workload, LRU): the form
+    settles within a few dozen frames and never goes back to timing (-1) afterwards,
+    and every launch still gives the counting form's bits."""
+    import torch
+    from vct import scenes
+    from vct.camera import Camera
+    ctx, s, arrs, (g0, E) = gpu_pipeline(128, "atrium")
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    cams = [Camera(), Camera(position=(0.1, 0.0, 2.6), yaw=-95.0)]
+    work = []
+    for w, h in ((320, 200), (256, 128)):
+        for cam in cams:                                   # two G-buffers per size (double buffering)
+            gb = [torch.empty((h, w, 4), device=dev) for _ in range(3)]
+            ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)
+            ref_d, ref_s = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+            cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            ctx.trace_device(*gb, w, h, cam.position, ref_d, ref_s, cone_steps=cnt)
+            work.append((w, h, cam, gb, ref_d, ref_s, cnt))
+    forms = {}
+    for i in range(160):
+        w, h, cam, gb, ref_d, ref_s, cnt = work[i % len(work)]
+        d, sp = torch.full_like(ref_d, -1.0), torch.full_like(ref_s, -1.0)
+        if i % 3 == 2:                                     # a counting launch in between
+            ctx.trace_device(*gb, w, h, cam.position, d, sp, cone_steps=cnt)
+        else:
+            ctx.trace_device(*gb, w, h, cam.position, d, sp)
+        torch.cuda.synchronize()
+        assert torch.equal(d, ref_d) and torch.equal(sp, ref_s), f"launch {i}"
+        f = ctx.trace_form
+        key = (w, h)
+        if key in forms:
+            assert f == forms[key], f"workload {key} went back to timing at launch {i}: {f}"
+        elif f >= 0 and i >= 2 * len(work):
+            forms[key] = f
+    assert set(forms) == {(320, 200), (256, 128)}, forms
+
+
+@pytest.mark.gpu
+def test_trace_form_forced_reports_candidate(gpu_ready):
+    """A variant that fixes both dimensions reports the forced candidate (not a stale one)."""
+    import torch
+    from vct import scenes
+    from vct._lib import VctTraceArgs  # noqa: F401  (the binding's struct)
+    from vct.camera import Camera
+    ctx, s, arrs, (g0, E) = gpu_pipeline(64, "cornell")
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    cam = Camera()
+    w, h = 128, 96
+    gb = [torch.empty((h, w, 4), device=dev) for _ in range(3)]
+    ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)
+    d, sp = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+    for variant, form in ((0x2000000 | 0x4000000, 1), (0x1000000 | 0x4000000, 0), (0x1000000 | 0x8000, 2)):
+        ctx.trace_device(*gb, w, h, cam.position, d, sp, variant=variant)
+        torch.cuda.synchronize()
+        assert ctx.trace_form == form, (hex(variant), ctx.trace_form)

@@ -145,7 +145,7 @@ def test_textured_trace_bitexact(gpu_ready, oracle_mod):
     ctx.composite_device(*gb, d, sp, w, h, scenes.LIGHT_DIR, out_linear4=lin)
     torch.cuda.synchronize()
     l_ref, _ = oracle_mod.composite(n, g0, E, ref_grid["albedo_occ"], pos, nrm, alb, got["diffuse"], got["spec"],
-                                    np.asarray(scenes.LIGHT_DIR, np.float32) / np.linalg.norm(scenes.LIGHT_DIR))
+                                    scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
     assert np.array_equal(lin.cpu().numpy(), l_ref)
     ctx.close()
 

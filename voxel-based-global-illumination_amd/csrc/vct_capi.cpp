@@ -205,7 +205,9 @@ vct_status vct_create_multi(const vct_config* cfg, uint32_t n_devices, vct_ctx**
 }
 
 uint32_t vct_num_devices(const vct_ctx* c) { return c ? 1u + (uint32_t)c->peers.size() : 0u; }
-int32_t vct_trace_form(const vct_ctx* c) { return c ? c->k4tune.chosen : -1; }
+int32_t vct_trace_form(const vct_ctx* c) {
+    return (c && c->k4tune.cur >= 0) ? c->k4tune.e[c->k4tune.cur].chosen : -1;
+}
 
 void vct_destroy(vct_ctx* c) {
     if (!c) return;
@@ -234,10 +236,11 @@ void vct_destroy(vct_ctx* c) {
     for (auto& s : c->scratch)
         if (s.p) (void)hipFree(s.p);
     if (c->ev) (void)hipEventDestroy(c->ev);
-    for (auto& f : c->k4tune.ev)
-        for (auto& sl : f)
-            for (hipEvent_t e : sl)
-                if (e) (void)hipEventDestroy(e);
+    for (auto& en : c->k4tune.e)
+        for (auto& f : en.ev)
+            for (auto& sl : f)
+                for (hipEvent_t e : sl)
+                    if (e) (void)hipEventDestroy(e);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -6,6 +6,7 @@
 #include <vector>
 #include "../../include/vct.h"
 #include "vct_device.h"
+#include "vct_variants.h"
 
 namespace vct {
 
@@ -60,25 +61,53 @@ struct Scratch {
 // surfaces, where a wave's lanes straddle an axis) and the occupancy form (5 waves/SIMD,
 // three-face bricks; pays on flat ones); a one-rank full frame may also be traced in
 // screen order or with ray reordering (pays on incoherent G-buffers).  Candidate
-// c = form | reordered << 1, over the dimensions the variant leaves free.  A context times both on its first timed launches of a
-// workload (HIP events on its stream; while timing, a launch first waits for the previous
-// timed one to finish, so the choice is made within 7 launches even when the host queues
-// frames far ahead), keeps the faster one, and re-times after kRetune launches or when
-// the workload changes.
+// c = form | reordered << 1, over the dimensions the variant leaves open.
+//
+// One entry per workload (frame size, tiling, cone set, grid size, forced bits), kept in
+// a small LRU table so that a host alternating workloads (two G-buffers, counting and
+// plain launches, two frame sizes) keeps every choice.  A new entry times each candidate
+// on its first counter-free launches (HIP events on the ctx stream; while timing, a
+// launch first waits for the previous timed launch of that entry, so the choice is made
+// within ~7 launches even when the host queues frames far ahead), then keeps the
+// fastest.  After that the launch path never blocks: every kWatchEvery-th launch of the
+// chosen candidate is timed with an event pair polled by hipEventQuery.  The entry times
+// its candidates again only when (a) kDriftRuns consecutive samples run more than kDrift
+// times the settled time (the G-buffer or the scene changed what is fastest: every
+// candidate is timed), or (b) a new voxelization (scene) has happened and the entry has
+// run kEpochMin launches since its last timing: then only the candidates within
+// kCompetitive of the previous winner are timed, so a candidate known to be much slower
+// (screen order on an incoherent G-buffer: 6x) never runs in steady state.
 struct K4Tuner {
-    static constexpr int kSlots = 4;          // event pairs in flight per form
-    static constexpr int kSamples = 2;        // timed samples per form after the first (cold) one
-    static constexpr uint32_t kRetune = 4096;
-    uint64_t key = ~0ull;                     // workload the state belongs to
-    int chosen = -1;                          // the candidate kept; -1 still timing
-    uint32_t since = 0;                       // timed launches since the choice
-    uint32_t launches = 0;                    // timed launches while choosing
-    hipEvent_t ev[4][kSlots][2] = {};
-    bool busy[4][kSlots] = {};
-    int head[4] = {0, 0, 0, 0};
-    int seen[4] = {0, 0, 0, 0};               // completed samples (the first one is dropped)
-    float best[4] = {0.0f, 0.0f, 0.0f, 0.0f}; // fastest completed sample, ms
-    hipEvent_t last = nullptr;                // end event of the previous timed launch while timing
+    static constexpr int kSlots = 4;          // event pairs in flight per candidate
+    static constexpr int kSamples = 2;        // timed samples per candidate after the first (cold) one
+    static constexpr int kEntries = 4;        // workloads remembered (LRU)
+    static constexpr uint32_t kWatchEvery = 16;
+    static constexpr int kDriftRuns = 3;
+    static constexpr float kDrift = 1.35f;
+    static constexpr uint32_t kEpochMin = 16;
+    static constexpr float kCompetitive = 1.5f;
+    struct Entry {
+        uint64_t key = ~0ull;                 // workload the entry belongs to
+        uint64_t used = 0;                    // LRU stamp
+        int chosen = -1;                      // the candidate kept; -1 still timing
+        float settled = 0.0f;                 // chosen candidate's time when it was chosen, ms
+        int drift = 0;                        // consecutive slow watch samples
+        uint32_t since = 0;                   // launches since the choice
+        uint32_t launches = 0;                // timed launches while choosing
+        uint32_t retimes = 0;                 // re-timings after the first choice
+        uint32_t epoch = 0;                   // vct_ctx::grid_epoch the choice was made on
+        bool limited = false;                 // this timing skips the candidates in `skip`
+        bool skip[4] = {false, false, false, false};
+        hipEvent_t ev[4][kSlots][2] = {};
+        bool busy[4][kSlots] = {};
+        int head[4] = {0, 0, 0, 0};
+        int seen[4] = {0, 0, 0, 0};           // completed samples (the first one is dropped)
+        float best[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // fastest completed sample, ms
+        hipEvent_t last = nullptr;            // end event of the previous timed launch while timing
+    };
+    Entry e[kEntries];
+    int cur = -1;                             // entry of the last launch (vct_trace_form)
+    uint64_t clock = 0;
 };
 
 }  // namespace vct
@@ -106,6 +135,7 @@ struct vct_ctx {
     hipEvent_t ev = nullptr;            // cross-device ordering of the multi-device calls
     void* comm = nullptr;               // RCCL communicator of vct_comm_init (ncclComm_t), one process per GPU
     int comm_rank = 0, comm_size = 1;
+    uint32_t comm_timeout_ms = 300000;  // deadline of every blocking step of vct_comm_* (vct_comm_set_timeout)
     bool own_stream = false;            // stream created by vct_create_multi (destroyed with the ctx)
     std::string err;
 };

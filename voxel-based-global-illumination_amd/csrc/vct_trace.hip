@@ -1370,42 +1370,102 @@ constexpr uint32_t kSplit3MaxBlocks = 1024;   // measured: 3 parts pay off at 10
 
 // The candidate of a default-variant launch (K4Tuner in vct_internal.h): bit 0 the
 // form (0 union, 1 occupancy), bit 1 ray reordering.  cands lists the candidates the
-// variant leaves open (n of them, 1, 2 or 4).  Timed (counter-free) launches cycle
-// through them until each has kSamples completed samples after its first (cold) one,
-// then the fastest is kept; counting launches take the choice (cands[0] while timing)
-// and are never timed.  *evp: the event pair to record around a timed launch, or null.
-static int k4_form(vct_ctx* c, uint64_t key, const int* cands, int n, bool timed, hipEvent_t** evp) {
-    K4Tuner& t = c->k4tune;
-    *evp = nullptr;
-    if (n == 1) return cands[0];
-    if (t.key != key) {                          // a new workload: its samples start afresh
-        t.key = key;
-        t.chosen = -1;
-        t.since = t.launches = 0;
-        for (int f = 0; f < 4; ++f) {
-            t.seen[f] = 0;
-            t.best[f] = 0.0f;
-            for (bool& b : t.busy[f]) b = false; // launches of the old workload still in flight: not its samples
-        }
+// variant leaves open (n of them, 1, 2 or 4).  While an entry is timing, timed
+// (counter-free) launches cycle through the candidates until each has kSamples
+// completed samples after its first (cold) one, then the fastest is kept; counting
+// launches take the choice (cands[0] while timing) and are never timed.  Once chosen,
+// every kWatchEvery-th timed launch is watched without blocking (drift check).
+// *evp: the event pair to record around the launch, or null.
+static void k4_retime(K4Tuner::Entry& t, bool limited) {
+    // limited: keep only the candidates within kCompetitive of the previous winner
+    for (int f = 0; f < 4; ++f) {
+        t.skip[f] = limited && t.chosen >= 0 && t.seen[f] > K4Tuner::kSamples &&
+                    t.best[f] > K4Tuner::kCompetitive * t.best[t.chosen];
+        t.seen[f] = 0;
+        t.best[f] = 0.0f;
+        for (bool& b : t.busy[f]) b = false;     // watch samples in flight: not timing samples
     }
-    if (t.chosen < 0 && timed && t.last) {       // while timing: the previous timed launch first
+    t.limited = limited;
+    t.chosen = -1;
+    t.drift = 0;
+    t.since = t.launches = 0;
+    t.last = nullptr;
+    ++t.retimes;
+}
+
+static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool timed, hipEvent_t** evp) {
+    K4Tuner& T = c->k4tune;
+    *evp = nullptr;
+    int ix = -1;
+    for (int i = 0; i < K4Tuner::kEntries; ++i)
+        if (T.e[i].key == key) ix = i;
+    if (ix < 0) {                                // a new workload: the least recently used entry
+        ix = 0;
+        for (int i = 1; i < K4Tuner::kEntries; ++i)
+            if (T.e[i].used < T.e[ix].used) ix = i;
+        K4Tuner::Entry& e = T.e[ix];
+        e.key = key;
+        e.chosen = -1;
+        k4_retime(e, false);
+        e.retimes = 0;
+        e.epoch = c->grid_epoch;
+    }
+    K4Tuner::Entry& t = T.e[ix];
+    t.used = ++T.clock;
+    T.cur = ix;
+    if (n_in == 1) {                             // the variant forces the candidate
+        t.chosen = cands_in[0];
+        return cands_in[0];
+    }
+    if (t.chosen < 0 && timed && t.last) {       // while timing: this entry's previous timed launch first
         (void)hipEventSynchronize(t.last);
         t.last = nullptr;
     }
-    for (int f = 0; f < 4; ++f)                  // harvest completed samples
+    for (int f = 0; f < 4; ++f)                  // harvest completed samples (non-blocking)
         for (int sl = 0; sl < K4Tuner::kSlots; ++sl) {
             if (!t.busy[f][sl] || hipEventQuery(t.ev[f][sl][1]) != hipSuccess) continue;
             t.busy[f][sl] = false;
             float ms = 0.0f;
             if (hipEventElapsedTime(&ms, t.ev[f][sl][0], t.ev[f][sl][1]) != hipSuccess) continue;
+            if (t.chosen >= 0) {                 // a watch sample of the chosen candidate
+                if (f != t.chosen) continue;
+                if (t.settled <= 0.0f) t.settled = ms;   // chosen without timing: the first sample settles it
+                else t.drift = ms > K4Tuner::kDrift * t.settled ? t.drift + 1 : 0;
+                continue;
+            }
             if (t.seen[f]++ == 0) continue;      // the first launch of a candidate pays its code load
             t.best[f] = t.seen[f] == 2 ? ms : fminf(t.best[f], ms);
         }
+    if (t.chosen >= 0 && timed) {
+        if (t.drift >= K4Tuner::kDriftRuns) {
+            k4_retime(t, false);                 // the workload changed under the key: every candidate
+            t.epoch = c->grid_epoch;
+        } else if (t.epoch != c->grid_epoch && t.since >= K4Tuner::kEpochMin) {
+            k4_retime(t, true);                  // a new scene: the competitive candidates only
+            t.epoch = c->grid_epoch;
+        }
+    }
+    // the candidates of this timing
+    int cands[4], n = 0;
+    for (int i = 0; i < n_in; ++i)
+        if (!(t.limited && t.skip[cands_in[i]])) cands[n++] = cands_in[i];
+    if (n == 0) cands[n++] = cands_in[0];
+    if (t.chosen < 0 && n == 1) {                // one competitive candidate left: nothing to time
+        t.chosen = cands[0];
+        t.settled = 0.0f;
+        t.since = 0;
+        return t.chosen;
+    }
     if (t.chosen >= 0) {
-        if (!timed || ++t.since < K4Tuner::kRetune) return t.chosen;
-        t.chosen = -1;                           // re-time: the frames may have changed
-        t.since = t.launches = 0;
-        for (int f = 0; f < 4; ++f) { t.seen[f] = 0; t.best[f] = 0.0f; }
+        if (!timed || ++t.since % K4Tuner::kWatchEvery != 0) return t.chosen;
+        const int f = t.chosen, sl = t.head[f];
+        if (t.busy[f][sl]) return f;
+        for (hipEvent_t& ev : t.ev[f][sl])
+            if (!ev && hipEventCreate(&ev) != hipSuccess) return f;
+        t.busy[f][sl] = true;
+        t.head[f] = (sl + 1) % K4Tuner::kSlots;
+        *evp = t.ev[f][sl];
+        return f;
     }
     bool done = true;
     for (int i = 0; i < n; ++i) done = done && t.seen[cands[i]] > K4Tuner::kSamples;
@@ -1414,6 +1474,10 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands, int n, bool timed
         for (int i = 1; i < n; ++i)
             if (t.best[cands[i]] < t.best[b]) b = cands[i];
         t.chosen = b;
+        t.settled = t.best[b];
+        t.since = 0;
+        for (int f = 0; f < 4; ++f)              // samples still in flight belong to the timing
+            for (bool& bz : t.busy[f]) bz = false;
         return t.chosen;
     }
     if (!timed) return cands[0];
@@ -1488,21 +1552,22 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     hipEvent_t* ev = nullptr;
     {
         int forms[2], nf = 0, orders[2], no = 0;
-        if (a->variant & 0x1000000) forms[nf++] = 0;
-        else if (a->variant & 0x2000000) forms[nf++] = 1;
+        if (a->variant & VCT_VARIANT_FORCE_UNION) forms[nf++] = 0;
+        else if (a->variant & VCT_VARIANT_FORCE_OCCUPANCY) forms[nf++] = 1;
         else { forms[nf++] = 0; forms[nf++] = 1; }
-        if (!can_reorder || (a->variant & 0x4000000)) orders[no++] = 0;
-        else if ((a->variant & 0x8000) || !deflt) orders[no++] = (a->variant & 0x8000) ? 1 : 0;
+        if (!can_reorder || (a->variant & VCT_VARIANT_SCREEN_ORDER)) orders[no++] = 0;
+        else if ((a->variant & VCT_VARIANT_REORDER) || !deflt) orders[no++] = (a->variant & VCT_VARIANT_REORDER) ? 1 : 0;
         else { orders[no++] = 0; orders[no++] = 1; }
         if (deflt) {
             int cands[4], n = 0;
             for (int o = 0; o < no; ++o)
                 for (int f = 0; f < nf; ++f) cands[n++] = forms[f] | orders[o] << 1;
-            uint64_t key = 1469598103934665603ull;   // FNV-1a over the workload
+            // FNV-1a over the workload: not the buffers, the scene or the counters (a changed
+            // scene or G-buffer under the same key is caught by the drift watch)
+            uint64_t key = 1469598103934665603ull;
             for (uint64_t v : {(uint64_t)a->width, (uint64_t)a->height, (uint64_t)k.rank, (uint64_t)k.world,
-                               (uint64_t)k.compact, (uint64_t)k.split, (uint64_t)c->cfg.n_diffuse, (uint64_t)k.spec_on,
-                               (uint64_t)g.n, (uint64_t)c->grid_epoch, (uint64_t)(a->variant & 0x7ffff00u),
-                               (uint64_t)(uintptr_t)a->pos4})   // another G-buffer: time again
+                               (uint64_t)k.compact, (uint64_t)c->cfg.n_diffuse, (uint64_t)k.spec_on, (uint64_t)g.n,
+                               (uint64_t)(a->variant & 0x7ffff00u)})
                 key = (key ^ v) * 1099511628211ull;
             cand = k4_form(c, key, cands, n, !cnt_form, &ev);
         } else {

@@ -30,7 +30,7 @@ from . import _lib
 from ._lib import VCT_ALL_RANKS, VctCamera, VctCommId, VctConfig, VctTexture, VctTraceArgs
 
 __all__ = ["Context", "VctError", "VctConfig", "VctCamera", "tiles_for_rank", "tile_offset", "VERTEX_FLOATS",
-           "VCT_ALL_RANKS"]
+           "VCT_ALL_RANKS", "comm_frame_layout"]
 
 VERTEX_FLOATS = 14          # reference Vertex: Position, Normal, TexCoords, Tangent, Bitangent
 VERTEX_STRIDE = VERTEX_FLOATS * 4
@@ -337,6 +337,14 @@ class Context:
     def comm_destroy(self):
         self._check(self.lib.vct_comm_destroy(self.h), "comm_destroy")
 
+    def comm_set_timeout(self, timeout_ms: int):
+        self._check(self.lib.vct_comm_set_timeout(self.h, int(timeout_ms)), "comm_set_timeout")
+
+    def comm_synchronize(self):
+        """Wait for the queued work incl. collectives; VctError(ECOMM) after the deadline."""
+        self._check(self.lib.vct_comm_synchronize(self.h), "comm_synchronize")
+
+
     def _gbuf_ptrs(self, width, height, pos4, nrm4, alb4):
         n = 4 * width * height
         return self._dev(pos4, "pos4", _F32, n), self._dev(nrm4, "nrm4", _F32, n), self._dev(alb4, "alb4", _F32, n)
@@ -411,3 +419,14 @@ class Context:
         counts = np.empty((n ** 3,), np.uint32)
         self._check(self.lib.vct_download_accum(self.h, _fptr(sums), _fptr(counts)), "download_accum")
         return sums, counts
+
+
+def comm_frame_layout(w: int, h: int, nranks: int, rank: int, root: int, lib=None) -> dict:
+    """vct_comm_frame_layout: where rank's tiles sit in the frame exchange buffer."""
+    from ._lib import VctCommLayout
+    lib = lib if lib is not None else _lib.load()
+    out = VctCommLayout()
+    st = lib.vct_comm_frame_layout(w, h, nranks, rank, root, C.byref(out))
+    if st != 0:
+        raise VctError(st, "vct_comm_frame_layout")
+    return {f: int(getattr(out, f)) for f, _ in VctCommLayout._fields_}

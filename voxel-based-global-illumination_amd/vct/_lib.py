@@ -20,7 +20,8 @@ EXPORTS = (
     "vct_inject_directional", "vct_build_mips", "vct_trace", "vct_trace_device",
     "vct_tiles_for_rank", "vct_untile_device", "vct_untile_planes_device", "vct_untile_planes_packed_device",
     "vct_tile_offset", "vct_comm_get_id", "vct_comm_init", "vct_comm_rank", "vct_comm_broadcast_level0",
-    "vct_comm_trace_frame", "vct_comm_destroy", "vct_gbuffer_raycast_device", "vct_gbuffer_raster_device",
+    "vct_comm_trace_frame", "vct_comm_destroy", "vct_comm_set_timeout", "vct_comm_synchronize",
+    "vct_comm_frame_layout", "vct_gbuffer_raycast_device", "vct_gbuffer_raster_device",
     "vct_composite_device",
     "vct_num_levels", "vct_level_dims", "vct_download_level", "vct_upload_level0",
     "vct_level0_device", "vct_copy_level0_to_device", "vct_set_level0_from_device",
@@ -63,6 +64,11 @@ class VctCommId(C.Structure):
 
 
 VCT_ALL_RANKS = -1
+
+
+class VctCommLayout(C.Structure):
+    _fields_ = [("buffer_tiles", C.c_uint64), ("diffuse_tile", C.c_uint64), ("spec_tile", C.c_uint64),
+                ("tiles", C.c_uint32), ("exchange_tiles", C.c_uint32)]
 
 
 class VctTraceArgs(C.Structure):
@@ -139,6 +145,9 @@ def bind(lib: C.CDLL) -> C.CDLL:
         "vct_comm_broadcast_level0": (i32, [P, u32]),
         "vct_comm_trace_frame": (i32, [P, C.POINTER(VctTraceArgs), i32]),
         "vct_comm_destroy": (i32, [P]),
+        "vct_comm_set_timeout": (i32, [P, u32]),
+        "vct_comm_synchronize": (i32, [P]),
+        "vct_comm_frame_layout": (i32, [u32, u32, u32, u32, i32, C.POINTER(VctCommLayout)]),
         "vct_gbuffer_raycast_device": (i32, [P, C.POINTER(VctCamera), u32, u32, f32, P, P, P]),
         "vct_gbuffer_raster_device": (i32, [P, C.POINTER(VctCamera), u32, u32, f32, P, P, P]),
         "vct_composite_device": (i32, [P, P, P, P, P, P, u32, u32, C.POINTER(f32), C.POINTER(f32), P, P]),

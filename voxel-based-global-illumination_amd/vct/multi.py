@@ -248,6 +248,24 @@ class FrameTracer:
             self._untile(b)
 
 
+def share_comm_id(dist, rank: int, root: int = 0, get_id=None) -> bytes:
+    """The vct_comm_* bootstrap for processes that already share a torch.distributed
+    group: rank `root` makes the ncclUniqueId (vct_comm_get_id, or `get_id()`), every
+    rank receives its 128 bytes by broadcast_object_list (works over gloo and RCCL)."""
+    if rank == root:
+        if get_id is None:
+            from . import Context
+            get_id = Context.comm_get_id
+        obj = [bytes(get_id())]
+    else:
+        obj = [None]
+    dist.broadcast_object_list(obj, src=root)
+    cid = obj[0]
+    if not isinstance(cid, (bytes, bytearray)) or len(cid) != 128:
+        raise ValueError(f"comm id: expected 128 bytes, got {type(cid).__name__} of {len(cid) if cid else 0}")
+    return bytes(cid)
+
+
 class PatternContext:
     """Stand-in for a vct Context in multi-rank rehearsals without a GPU
     (bench.py --dry-run, tests): its "trace" writes each owned pixel's frame index
