@@ -26,14 +26,25 @@ the exchange alone are reported beside the metric.
 value = cone steps of the frame (counted by the kernel; identical to the
 oracle's count, tests/test_parity_gpu.py) x K / max-over-ranks wall time.
 
-roofline: K4 is bound by instruction issue, not HBM.  The
-binding figure is the VALU issue rate: SQ_INSTS_VALU per launch (rocprofv3 PMC,
-profiles/k4_counters.json, valid only for the library build it was measured
-on: the file records the .so's sha256) / the live K4 time, against 1024 SIMDs x
-2.4 GHz / 2 cycles per wave64 VALU instruction.  Beside it: the measured HBM
-traffic (2 FETCH_SIZE + WRITE_SIZE, gfx950 correction) against 8 TB/s, the
-scalar issue rate, and the spec's algorithmic texel bytes (`gather_bytes`,
-served ~99 % by LDS / L1 / L2).
+roofline: K4 is bound by instruction issue, not HBM.  From
+the PMC record of the timed K4 form (rocprofv3, profiles/k4_counters.json, valid
+only for the library build it was measured on: the file records the .so's
+sha256) three rates are formed over the live K4 time -- VALU issue
+(SQ_INSTS_VALU against 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction),
+scalar issue (SQ_INSTS_SALU against 256 CUs x 2.4 GHz) and the measured HBM
+traffic (2 FETCH_SIZE + WRITE_SIZE, gfx950 correction, against 8 TB/s) -- and
+`roofline` names the most loaded one (`bound`).  The spec's algorithmic texel
+bytes (`gather_bytes`, served ~99 % by LDS / L1 / L2) are reported beside them.
+At N > 1 the record is the one of a rank's own launch (`ranksN` keys, measured
+by tools/rank_emul.py under rocprofv3).
+
+Beside the metric (rank 0's JSON line): `frame_loop` (N = 1: 5000 default-variant
+frames of G_scene and of G_rand after their choice settled: per-frame K4 time and
+host launch time, the tuner's hitch check), `multi_config` (BASELINE configs[3]
+and [4]: atrium 512^3 at 3840x2160 with 9+1 cones at every N, its 2 GiB level-0
+broadcast timed; courtyard 512^3, 16+1 cones, 4K at N = 1 and 8) and, at N > 1
+over RCCL, `capi` (one frame assembled through the torch-free C-ABI path,
+vct_comm_*: checked bit-equal to the torch frame and timed).
 
 `--gpus N` without WORLD_SIZE in the environment starts the N ranks itself
 (one child process per GPU, before anything touches a GPU).  `--dry-run`
@@ -92,6 +103,10 @@ def parse():
     p.add_argument("--stress", default="rand",
                    help="N = 1: also time the cache-hostile G_rand G-buffer on the metric scene, screen "
                         "order vs ray reordering (empty or 'none': skip)")
+    p.add_argument("--frame-loop", type=int, default=5000,
+                   help="N = 1: frames of the steady-state hitch loop per G-buffer (0: skip)")
+    p.add_argument("--multi-config", default="c4,c5",
+                   help="BASELINE configs[3] / [4] measured beside the metric (comma list; empty or 'none': skip)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-json", default=PROFILE)
@@ -225,8 +240,46 @@ def host_info():
     except OSError:
         pass
     omp = os.environ.get("OMP_NUM_THREADS")
+    quota, raw = cgroup_cpus()
     return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
-            "omp_num_threads": int(omp) if omp and omp.isdigit() else None}
+            "omp_num_threads": int(omp) if omp and omp.isdigit() else None,
+            "cgroup_cpu_max": raw, "cgroup_cpus": quota}
+
+
+def cgroup_cpus():
+    """CPUs the job's cgroup may use: cgroup v2 cpu.max (quota period) or v1
+    cfs_quota_us / cfs_period_us; (None, raw) when there is no quota."""
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.max"):
+        try:
+            raw = open(path).read().strip()
+        except OSError:
+            continue
+        q, _, per = raw.partition(" ")
+        if q == "max" or not per:
+            return None, raw
+        return max(1, math.ceil(int(q) / int(per))), raw
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        raw = f"cfs_quota_us={q} cfs_period_us={per}"
+        return (max(1, math.ceil(q / per)) if q > 0 else None), raw
+    except (OSError, ValueError):
+        return None, None
+
+
+def cpu_share(host):
+    """Threads for the CPU baseline and why: the cgroup quota if there is one (capped by
+    the affinity mask); else the pool's documented per-GPU share, which the pool exports
+    as OMP_NUM_THREADS (16 per GPU on the MI355X boxes, whose affinity mask and
+    os.cpu_count() show the whole machine); else the affinity mask."""
+    aff = host["affinity_cpus"] or os.cpu_count() or 1
+    if host["cgroup_cpus"]:
+        return min(host["cgroup_cpus"], aff), f"cgroup quota {host['cgroup_cpu_max']}"
+    if host["omp_num_threads"]:
+        return min(host["omp_num_threads"], aff), (
+            f"no cgroup CPU quota ({host['cgroup_cpu_max'] or 'cpu.max absent'}); the GPU pool's per-GPU CPU "
+            f"share, exported as OMP_NUM_THREADS={host['omp_num_threads']} (the affinity mask lists {aff})")
+    return aff, "affinity mask (no cgroup quota, no OMP_NUM_THREADS)"
 
 
 def cpu_baseline(ctx, n, g0, E, gb_host, eye, n_diffuse, spec, steps_px_gpu, target_s):
@@ -242,10 +295,8 @@ def cpu_baseline(ctx, n, g0, E, gb_host, eye, n_diffuse, spec, steps_px_gpu, tar
             parts.append(ctx.download_level(l, f).ravel())
     pyr = np.concatenate(parts)
     host = host_info()
-    # threads: the CPU share the pool gives this job (OMP_NUM_THREADS, 16 per GPU on the
-    # MI355X boxes, whose affinity mask shows the whole 256-thread machine), else every
-    # core in the affinity mask
-    cores = host["omp_num_threads"] or host["affinity_cpus"] or os.cpu_count() or 1
+    cores, basis = cpu_share(host)
+    host["cores_basis"] = basis
     probe_step = 128
     t0 = time.perf_counter()
     O.trace(n, g0, E, r0, pyr, pos, nrm, alb, eye, aniso=True, n_diffuse=n_diffuse, specular=spec,
@@ -350,6 +401,17 @@ def dry_run(args, world):
         dist.destroy_process_group()
 
 
+_SCENES = {}
+
+
+def scene_arrays(name):
+    """vct.scenes arrays, built once per process (the 1 M-triangle courtyard takes seconds)"""
+    if name not in _SCENES:
+        from vct import scenes
+        _SCENES[name] = scenes.SCENES[name]().arrays()
+    return _SCENES[name]
+
+
 def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, counting_only=False):
     """K1-K3 for `scene_name`, the G-buffer, one counting frame, then K timed frames."""
     import numpy as np
@@ -365,8 +427,7 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
         torch.cuda.synchronize()
         return (time.perf_counter() - t) * 1e3
 
-    scene = scenes.SCENES[scene_name]()
-    v, i, m, k = scene.arrays()
+    v, i, m, k = scene_arrays(scene_name)
     # K1 on every rank (each process holds the scene, as the reference's loader does),
     # from device-resident geometry (the reference's meshes live in GL buffers);
     # K1-K3 are timed on a second call (the first one allocates their scratch)
@@ -485,6 +546,14 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     return r
 
 
+def form_name(f):
+    """vct_trace_form -> its description (None while timing)"""
+    if f is None or f < 0:
+        return None
+    return ("occupancy, 5 waves/SIMD" if f & 1 else "four-face union, 4 waves/SIMD") + (
+        ", ray reordering" if f & 2 else ", screen order")
+
+
 def settle_form(ctx, torch, launch, max_launches=24):
     """Launch until the context has chosen its K4 form for this workload; returns it."""
     for _ in range(max_launches):
@@ -493,6 +562,143 @@ def settle_form(ctx, torch, launch, max_launches=24):
         if ctx.trace_form >= 0:
             break
     return ctx.trace_form
+
+
+def frame_loop(torch, ctx, gb, w, h, eye, stream, frames, variant=0):
+    """A renderer's steady state: `frames` default-variant frames on one G-buffer after
+    the context's choice for it has settled.  Per frame: the K4 time on the stream
+    (events) and the host time of the trace call (a launch path that blocked on the GPU
+    would show here).  The tuner watches every 16th launch without blocking and times
+    again only on a drift (vct_trace_form), so max / median stays near 1."""
+    import numpy as np
+    d, sp = torch.empty((h, w, 4), device=gb[0].device), torch.empty((h, w, 4), device=gb[0].device)
+    launch = lambda: ctx.trace_device(*gb, w, h, eye, d, sp, variant=variant)   # noqa: E731
+    settle = 0
+    for settle in range(1, 65):
+        launch()
+        torch.cuda.synchronize()
+        if ctx.trace_form >= 0:
+            break
+    for _ in range(4):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(frames)]
+    host = np.empty(frames)
+    forms = set()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(frames):
+        ev[i][0].record(stream)
+        t = time.perf_counter()
+        launch()
+        host[i] = time.perf_counter() - t
+        ev[i][1].record(stream)
+        if i % 250 == 0:
+            forms.add(ctx.trace_form)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    forms.add(ctx.trace_form)
+    ms = np.array([a.elapsed_time(b) for a, b in ev])
+    med = float(np.median(ms))
+    return {"frames": frames, "settle_launches": settle, "k4_ms_median": round(med, 4),
+            "k4_ms_p99": round(float(np.percentile(ms, 99)), 4), "k4_ms_max": round(float(ms.max()), 4),
+            "max_over_median": round(float(ms.max()) / med, 3),
+            "host_launch_ms_median": round(float(np.median(host)) * 1e3, 4),
+            "host_launch_ms_max": round(float(host.max()) * 1e3, 4), "wall_ms_per_frame": round(wall / frames * 1e3, 4),
+            "forms_seen": sorted(form_name(f) or "timing" for f in forms)}
+
+
+MULTI_CONFIGS = {
+    # BASELINE.json configs[3]: "Sponza, 512^3 grid, 4K framebuffer, screen tiles across 2/4/8 MI355X with RCCL grid bcast"
+    "c4": {"scene": "atrium", "n": 512, "width": 3840, "height": 2160, "n_diffuse": 9, "ranks": None},
+    # configs[4]: "San Miguel, 512^3 6-face anisotropic grid, 16 cones, 4K, 8 MI355X" (+ one GPU for the curve)
+    "c5": {"scene": "courtyard", "n": 512, "width": 3840, "height": 2160, "n_diffuse": 16, "ranks": (1, 8)},
+}
+
+
+def measure_config(args, torch, dist, rank, world, dev, stream, cfg):
+    """One BASELINE configuration beside the metric: its own context, K1-K3, the level-0
+    broadcast (N > 1, timed), the pipelined frame loop, the slowest rank's trace."""
+    import copy
+    from vct import Context, scenes
+    a = copy.copy(args)
+    a.n, a.width, a.height, a.n_diffuse, a.gbuffer = cfg["n"], cfg["width"], cfg["height"], cfg["n_diffuse"], "scene"
+    g0, E = scenes.grid_for_unit_box(a.n)
+    ctx = Context(a.n, g0, E, aniso=True, n_diffuse=a.n_diffuse, specular=not args.no_spec, device=dev.index)
+    ctx.set_stream(stream.cuda_stream)
+    m = measure_scene(a, torch, dist, ctx, cfg["scene"], rank, world, dev, stream)
+    out = {"workload": f"{cfg['scene']}{STAND_IN.get(cfg['scene'], '')}, {a.n}^3 aniso RGBA32F, "
+                       f"{a.width}x{a.height}, {a.n_diffuse}+{0 if args.no_spec else 1} cones",
+           "value": round(m["value"], 2), "unit": "Mcone-steps/s", "ms_per_step": round(m["ms_per_step"], 4),
+           "frame_cone_steps": m["frame_cone_steps"], "k4_kernel_ms_avg_rank0": round(m["k4_kernel_ms_avg"], 4),
+           "k4_form_rank0": form_name(m["k4_form"])}
+    for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
+               "replicated_k2_equals_bcast", "trace_ms_max_rank", "gather_ms", "allgather_ms"):
+        if k_ in m:
+            out[k_] = m[k_]
+    if world > 1:
+        out["grid_bcast_GBs"] = round(a.n ** 3 * 16 / (m["grid_bcast_ms"] * 1e-3) / 1e9, 1) if m["grid_bcast_ms"] else None
+    del m
+    ctx.close()
+    torch.cuda.empty_cache()
+    return out
+
+
+def capi_leg(args, torch, dist, ctx, rank, world, dev, stream, gb, eye):
+    """N > 1 over RCCL: the torch-free C-ABI path (include/vct.h vct_comm_*, the one a
+    C++ host started once per GPU uses).  The ncclUniqueId goes from rank 0 to every
+    rank over the torch group (vct.multi.share_comm_id); level 0 is broadcast in place
+    (vct_comm_broadcast_level0, must leave the grid unchanged: every rank already holds
+    it); one frame is assembled on rank 0 (root 0: ncclSend/ncclRecv of packed tiles)
+    and on every rank (VCT_ALL_RANKS: one ncclAllGather), each checked bit-equal to the
+    torch FrameTracer's frame and timed over `steps` synchronous frames."""
+    from vct import VCT_ALL_RANKS
+    from vct.multi import FrameTracer, share_comm_id
+    w, h = args.width, args.height
+    ref = FrameTracer(ctx, torch, dist, w, h, rank, world, dev, mode="allgather")
+    ref_d, ref_s = ref.frame(gb, eye, variant=args.variant)
+    torch.cuda.synchronize()
+    cid = share_comm_id(dist, rank)
+    ctx.comm_set_timeout(120000)
+    ctx.comm_init(cid, world, rank)
+    n = ctx.n
+    before = torch.empty((n ** 3 * 4,), dtype=torch.float32, device=dev)
+    after = torch.empty_like(before)
+    ctx.copy_level0_to_device(before)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    ctx.comm_broadcast_level0(0)
+    ctx.comm_synchronize()
+    bcast_ms = (time.perf_counter() - t) * 1e3
+    ctx.copy_level0_to_device(after)
+    torch.cuda.synchronize()
+    bcast_ok = bool(torch.equal(before, after))
+    del before, after
+    ctx.build_mips()
+    out = {"bcast_equal": bcast_ok}
+    d, sp = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+    for root, name in ((0, "present"), (VCT_ALL_RANKS, "allgather")):
+        d.fill_(-1.0)
+        sp.fill_(-1.0)
+        ctx.comm_trace_frame(*gb, w, h, eye, d, sp, root=root, variant=args.variant)
+        ctx.comm_synchronize()
+        ok = True
+        if root == VCT_ALL_RANKS or rank == root:
+            ok = bool(torch.equal(d, ref_d) and torch.equal(sp, ref_s))
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.comm_trace_frame(*gb, w, h, eye, d, sp, root=root, variant=args.variant)
+        ctx.comm_synchronize()
+        ms = (time.perf_counter() - t) / args.steps * 1e3
+        bad, ms = max_over_ranks(torch, dist, dev, [0.0 if ok else 1.0, ms], world)
+        out[f"{name}_equal"] = bad == 0.0
+        out[f"{name}_frame_ms"] = round(ms, 4)
+    bad = max_over_ranks(torch, dist, dev, [0.0 if bcast_ok else 1.0, bcast_ms], world)
+    out["bcast_equal"], out["bcast_ms"] = bad[0] == 0.0, round(bad[1], 3)
+    ctx.comm_destroy()
+    return out
 
 
 def stress_rand(args, torch, ctx, dev, stream):
@@ -531,7 +737,8 @@ def stress_rand(args, torch, ctx, dev, stream):
     steps = int(cnt[0].item())
     (a0, a1), (b0, b1), (c0, c1) = outs.values()
     t0, t1, t2 = ms.values()
-    return {"gbuffer": "G_rand (seed 42), same grid", "frame_cone_steps": steps, "frames": reps,
+    loop = frame_loop(torch, ctx, gb, w, h, eye, stream, args.frame_loop, variant=auto) if args.frame_loop else None
+    return {"gbuffer": "G_rand (seed 42), same grid", "frame_cone_steps": steps, "frames": reps, "_loop": loop,
             "screen_order_ms": round(t0, 4), "reordered_ms": round(t1, 4), "default_ms": round(t2, 4),
             "screen_order_Mcone_steps_s": round(steps / t0 / 1e3, 2),
             "reordered_Mcone_steps_s": round(steps / t1 / 1e3, 2),
@@ -603,9 +810,7 @@ def run(args, world):
             result[k_] = m[k_]
         result["k4_kernel_ms_avg"] = round(m["k4_kernel_ms_avg"], 4)
         result["k4_kernel_ms_median"] = round(m["k4_kernel_ms_median"], 4)
-        f = m["k4_form"]
-        result["k4_form"] = None if f < 0 else ("occupancy, 5 waves/SIMD" if f & 1 else "four-face union, 4 waves/SIMD") + (
-            ", ray reordering" if f & 2 else ", screen order")
+        result["k4_form"] = form_name(m["k4_form"])
         for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
                    "frame_relight_bcast_ms", "frame_relight_replicated_ms", "replicated_k2_equals_bcast",
                    "trace_ms_max_rank", "gather_ms", "allgather_ms"):
@@ -613,15 +818,32 @@ def run(args, world):
                 result[k_] = m[k_]
         result["roofline"] = roof
         result["cpu_baseline"] = None
+        result["frame_loop"] = None
         if world == 1 and not args.no_cpu_baseline:
             host = tuple(t_.cpu().numpy() for t_ in m["_gb"])
             result["cpu_baseline"] = cpu_baseline(ctx, n, g0, E, host, m["_eye"], args.n_diffuse, spec,
                                                   m["_steps_px"].cpu().numpy().astype(np.uint32), args.cpu_seconds)
+    if world == 1 and args.frame_loop:
+        loop_scene = frame_loop(torch, ctx, m["_gb"], w, h, m["_eye"], stream, args.frame_loop, variant=args.variant)
+        result["frame_loop"] = {f"G_{args.gbuffer}": loop_scene}
+    capi = None
+    if world > 1:
+        if os.environ.get("VCT_DIST_BACKEND", "nccl") == "nccl":
+            capi = capi_leg(args, torch, dist, ctx, rank, world, dev, stream, m["_gb"], m["_eye"])
+        else:
+            capi = {"note": "skipped: the C-ABI RCCL path needs one GPU per rank (VCT_DIST_BACKEND is not nccl)",
+                    "present_equal": None, "allgather_equal": None, "bcast_equal": None,
+                    "present_frame_ms": None, "allgather_frame_ms": None, "bcast_ms": None}
+        if rank == 0:
+            result["capi"] = capi
     del m
     torch.cuda.empty_cache()
     st = (args.stress or "").strip()
     if st == "rand" and world == 1 and args.gbuffer == "scene":
         result["stress"] = stress_rand(args, torch, ctx, dev, stream)
+        loop = result["stress"].pop("_loop")
+        if loop is not None:
+            result["frame_loop"]["G_rand"] = loop
         torch.cuda.empty_cache()
     sec = (args.secondary or "").strip()
     if sec and sec != "none" and sec != args.scene:
@@ -632,12 +854,23 @@ def run(args, world):
                 "scene": sec + STAND_IN.get(sec, ""), "value": round(s2["value"], 2), "unit": "Mcone-steps/s",
                 "ms_per_step": round(s2["ms_per_step"], 4), "k4_kernel_ms_avg": round(s2["k4_kernel_ms_avg"], 4),
                 "frame_cone_steps": s2["frame_cone_steps"], "valid_px": s2["valid_px"],
-                "k1_voxelize_ms": s2["k1_voxelize_ms"], "k4_form": s2["k4_form"],
+                "k1_voxelize_ms": s2["k1_voxelize_ms"], "k4_form": form_name(s2["k4_form"]),
             }
             if "trace_ms_max_rank" in s2:
                 result["secondary"]["trace_ms_max_rank"] = s2["trace_ms_max_rank"]
         del s2
     ctx.close()
+    torch.cuda.empty_cache()
+    mc = [c.strip() for c in (args.multi_config or "").split(",") if c.strip() and c.strip() != "none"]
+    if mc:
+        out = {}
+        for name in mc:
+            cfg = MULTI_CONFIGS[name]
+            if cfg["ranks"] is not None and world not in cfg["ranks"]:
+                continue
+            out[name] = measure_config(args, torch, dist, rank, world, dev, stream, cfg)
+        if rank == 0:
+            result["multi_config"] = out
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:

@@ -7,6 +7,12 @@ For each world size N and each rank r < N, times exactly the launch rank r
 makes in the N-GPU bench (its interleaved 64x64 tiles, rank-compact output) and
 reports the slowest rank: the K4 part of the N-GPU step (the all-gather and
 the untile come on top; the gather overlaps the next frame's trace).
+
+    python tools/rank_emul.py --pmc-world N [--pmc-rank 0] [--pmc-launches 20]
+
+only repeats rank R's launch of the N-rank split (after the context settled its
+form for it), for rocprofv3 to record the per-rank PMC that bench.py's roofline
+uses at N > 1 (tools/k4_profile_ranks.sh -> profiles/k4_counters.json `ranksN`).
 """
 import argparse
 import json
@@ -26,6 +32,9 @@ def main():
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--variant", type=lambda x: int(x, 0), default=0)
     ap.add_argument("--scene", default="atrium")
+    ap.add_argument("--pmc-world", type=int, default=0)
+    ap.add_argument("--pmc-rank", type=int, default=0)
+    ap.add_argument("--pmc-launches", type=int, default=20)
     a = ap.parse_args()
     import torch
     from vct import Context, scenes
@@ -55,6 +64,22 @@ def main():
             ts.append(e0.elapsed_time(e1))
         return sorted(ts)[len(ts) // 2]
 
+    if a.pmc_world:
+        W, r = a.pmc_world, a.pmc_rank
+        maxt = tiles_for_rank(a.w, a.h, 0, W)
+        buf = torch.empty((2, maxt * TILE * TILE, 4), device=dev)
+        launch = lambda: ctx.trace_device(*gb, a.w, a.h, cam.position, buf[0], buf[1], tile_rank=r,  # noqa: E731
+                                          tile_world=W, tile_compact=W > 1, variant=a.variant)
+        for _ in range(64):
+            launch()
+            torch.cuda.synchronize()
+            if ctx.trace_form >= 0:
+                break
+        for _ in range(a.pmc_launches):
+            launch()
+        torch.cuda.synchronize()
+        print(json.dumps({"world": W, "rank": r, "form": ctx.trace_form, "launches": a.pmc_launches}))
+        return
     out = {}
     for W in [int(x) for x in a.worlds.split(",")]:
         maxt = tiles_for_rank(a.w, a.h, 0, W)
