@@ -554,12 +554,18 @@ def form_name(f):
         ", ray reordering" if f & 2 else ", screen order")
 
 
-def settle_form(ctx, torch, launch, max_launches=24):
-    """Launch until the context has chosen its K4 form for this workload; returns it."""
+def settle_form(ctx, torch, launch, stable=24, max_launches=256):
+    """Launch (one frame at a time) until the context's choice for this workload has held
+    for `stable` launches -- also when a choice made on another G-buffer or scene under
+    the same workload key is first re-timed by the drift watch; returns it."""
+    last, run = None, 0
     for _ in range(max_launches):
         launch()
         torch.cuda.synchronize()
-        if ctx.trace_form >= 0:
+        f = ctx.trace_form
+        run = run + 1 if (f >= 0 and f == last) else 0
+        last = f
+        if run >= stable:
             break
     return ctx.trace_form
 
@@ -573,25 +579,19 @@ def frame_loop(torch, ctx, gb, w, h, eye, stream, frames, variant=0):
     import numpy as np
     d, sp = torch.empty((h, w, 4), device=gb[0].device), torch.empty((h, w, 4), device=gb[0].device)
     launch = lambda: ctx.trace_device(*gb, w, h, eye, d, sp, variant=variant)   # noqa: E731
-    settle = 0
-    for settle in range(1, 65):
-        launch()
-        torch.cuda.synchronize()
-        if ctx.trace_form >= 0:
-            break
-    for _ in range(4):
-        launch()
+    settled = settle_form(ctx, torch, launch)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(frames)]
     host = np.empty(frames)
     forms = set()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(frames):
+    for i in range(frames):         # one frame in flight, as a renderer presents each frame
         ev[i][0].record(stream)
         t = time.perf_counter()
         launch()
         host[i] = time.perf_counter() - t
         ev[i][1].record(stream)
+        ev[i][1].synchronize()
         if i % 250 == 0:
             forms.add(ctx.trace_form)
     torch.cuda.synchronize()
@@ -599,7 +599,7 @@ def frame_loop(torch, ctx, gb, w, h, eye, stream, frames, variant=0):
     forms.add(ctx.trace_form)
     ms = np.array([a.elapsed_time(b) for a, b in ev])
     med = float(np.median(ms))
-    return {"frames": frames, "settle_launches": settle, "k4_ms_median": round(med, 4),
+    return {"frames": frames, "settled_form": form_name(settled), "k4_ms_median": round(med, 4),
             "k4_ms_p99": round(float(np.percentile(ms, 99)), 4), "k4_ms_max": round(float(ms.max()), 4),
             "max_over_median": round(float(ms.max()) / med, 3),
             "host_launch_ms_median": round(float(np.median(host)) * 1e3, 4),
@@ -723,7 +723,10 @@ def stress_rand(args, torch, ctx, dev, stream):
         sp = torch.empty((h, w, 4), device=dev)
         if v & 0x4000000:      # the counting pass, once (screen order)
             ctx.trace_device(*gb, w, h, eye, d, sp, cone_steps=cnt, variant=v)
-        form[v] = settle_form(ctx, torch, lambda: ctx.trace_device(*gb, w, h, eye, d, sp, variant=v))
+        # a forced order holds at once; the default variant may first re-time the choice it made
+        # on G_scene under the same workload key (drift watch), so it settles longer
+        form[v] = settle_form(ctx, torch, lambda: ctx.trace_device(*gb, w, h, eye, d, sp, variant=v),
+                              stable=6 if v != auto else 24)
         ctx.trace_device(*gb, w, h, eye, d, sp, variant=v)     # warm
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         torch.cuda.synchronize()

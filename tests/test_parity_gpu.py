@@ -36,16 +36,21 @@ def test_voxelize_inject_mips_bitexact(gpu_ready, oracle_mod, name, n):
 
 
 @pytest.mark.parametrize("aniso", [True, False])
-def test_mips_bitexact_random_level0(gpu_ready, oracle_mod, aniso):
+@pytest.mark.parametrize("n", [4, 8, 32, 64, 128])
+def test_mips_bitexact_random_level0(gpu_ready, oracle_mod, aniso, n):
+    """K3 on random level 0: every size path of the launch plan (n = 4, 8: the fused tail
+    only; 32: one tail block per face; 64, 128: several tail blocks and the last-block
+    ticket), built twice (the per-face tickets reset) -- bit-exact vs the oracle."""
     from vct import Context
-    n = 32
-    rng = np.random.default_rng(3)
+    rng = np.random.default_rng(3 + n)
     a = (rng.random((n, n, n)) < 0.3).astype(np.float32)
     r0 = np.concatenate([rng.random((n, n, n, 3)).astype(np.float32) * a[..., None], a[..., None]], -1)
     ctx = Context(n, (0, 0, 0), 1.0, aniso=aniso)
     ctx.upload_level0(r0)
-    ctx.build_mips()
-    assert np.array_equal(gpu_pyramid_flat(ctx), oracle_mod.build_mips(n, r0, aniso))
+    ref = oracle_mod.build_mips(n, r0, aniso)
+    for _ in range(2):
+        ctx.build_mips()
+        assert np.array_equal(gpu_pyramid_flat(ctx), ref)
     ctx.close()
 
 

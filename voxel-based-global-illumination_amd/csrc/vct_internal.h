@@ -76,12 +76,15 @@ struct Scratch {
 // candidate is timed), or (b) a new voxelization (scene) has happened and the entry has
 // run kEpochMin launches since its last timing: then only the candidates within
 // kCompetitive of the previous winner are timed, so a candidate known to be much slower
-// (screen order on an incoherent G-buffer: 6x) never runs in steady state.
+// (screen order on an incoherent G-buffer: 6x) never runs in steady state.  A re-timing
+// keeps the first sample of each candidate (its code is loaded already) and drops a
+// candidate after one sample that is kCompetitive times slower than the best so far.
+// VCT_TUNE_LOG=1 prints every decision to stderr.
 struct K4Tuner {
     static constexpr int kSlots = 4;          // event pairs in flight per candidate
     static constexpr int kSamples = 2;        // timed samples per candidate after the first (cold) one
     static constexpr int kEntries = 4;        // workloads remembered (LRU)
-    static constexpr uint32_t kWatchEvery = 16;
+    static constexpr uint32_t kWatchEvery = 2;
     static constexpr int kDriftRuns = 3;
     static constexpr float kDrift = 1.35f;
     static constexpr uint32_t kEpochMin = 16;
@@ -101,7 +104,7 @@ struct K4Tuner {
         hipEvent_t ev[4][kSlots][2] = {};
         bool busy[4][kSlots] = {};
         int head[4] = {0, 0, 0, 0};
-        int seen[4] = {0, 0, 0, 0};           // completed samples (the first one is dropped)
+        int seen[4] = {0, 0, 0, 0};           // completed samples (the first one of a first timing is dropped)
         float best[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // fastest completed sample, ms
         hipEvent_t last = nullptr;            // end event of the previous timed launch while timing
     };
@@ -129,6 +132,7 @@ struct vct_ctx {
     unsigned* spec_keys = nullptr;      // [2 * kSpecSlots]: specular table keys (~0u free), then states
     vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)
     int* k1_err = nullptr;              // device flag of vct_voxelize_device (index out of range)
+    unsigned* k3_tickets = nullptr;     // [6] K3 tail: per-face workgroup tickets (0 between builds)
     // vct_create_multi: this context is device rank 0 and owns one context per
     // further device (ranks 1..n-1); empty for a single-device context
     std::vector<vct_ctx*> peers;

@@ -34,6 +34,9 @@
 //  and to the CPU oracle.
 #include <climits>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "vct_internal.h"
 
 // Debug-build counters (make dbg -> vct/libvct_hip_dbg.so, tools/dbg_counters.py):
@@ -1376,12 +1379,17 @@ constexpr uint32_t kSplit3MaxBlocks = 1024;   // measured: 3 parts pay off at 10
 // launches take the choice (cands[0] while timing) and are never timed.  Once chosen,
 // every kWatchEvery-th timed launch is watched without blocking (drift check).
 // *evp: the event pair to record around the launch, or null.
+static bool tune_log() {
+    static const bool on = getenv("VCT_TUNE_LOG") != nullptr;
+    return on;
+}
+
 static void k4_retime(K4Tuner::Entry& t, bool limited) {
     // limited: keep only the candidates within kCompetitive of the previous winner
     for (int f = 0; f < 4; ++f) {
         t.skip[f] = limited && t.chosen >= 0 && t.seen[f] > K4Tuner::kSamples &&
                     t.best[f] > K4Tuner::kCompetitive * t.best[t.chosen];
-        t.seen[f] = 0;
+        t.seen[f] = 1;                           // warm code: no cold sample to drop
         t.best[f] = 0.0f;
         for (bool& b : t.busy[f]) b = false;     // watch samples in flight: not timing samples
     }
@@ -1407,6 +1415,7 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
         e.key = key;
         e.chosen = -1;
         k4_retime(e, false);
+        for (int f = 0; f < 4; ++f) e.seen[f] = 0;   // first timing: drop each candidate's cold sample
         e.retimes = 0;
         e.epoch = c->grid_epoch;
     }
@@ -1434,13 +1443,24 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
                 continue;
             }
             if (t.seen[f]++ == 0) continue;      // the first launch of a candidate pays its code load
-            t.best[f] = t.seen[f] == 2 ? ms : fminf(t.best[f], ms);
+            t.best[f] = t.best[f] == 0.0f ? ms : fminf(t.best[f], ms);
         }
+    if (t.chosen < 0) {                          // a candidate clearly slower than the best so far: done
+        float lo = 0.0f;
+        for (int f = 0; f < 4; ++f)
+            if (t.best[f] > 0.0f && (lo == 0.0f || t.best[f] < lo)) lo = t.best[f];
+        for (int f = 0; f < 4; ++f)
+            if (t.best[f] > K4Tuner::kCompetitive * lo && t.seen[f] <= K4Tuner::kSamples) t.seen[f] = K4Tuner::kSamples + 1;
+    }
     if (t.chosen >= 0 && timed) {
         if (t.drift >= K4Tuner::kDriftRuns) {
+            if (tune_log())
+                fprintf(stderr, "[vct tune] key %016llx: drift of %d (settled %.4f ms): time again\n",
+                        (unsigned long long)t.key, t.chosen, t.settled);
             k4_retime(t, false);                 // the workload changed under the key: every candidate
             t.epoch = c->grid_epoch;
         } else if (t.epoch != c->grid_epoch && t.since >= K4Tuner::kEpochMin) {
+            if (tune_log()) fprintf(stderr, "[vct tune] key %016llx: new scene: time again\n", (unsigned long long)t.key);
             k4_retime(t, true);                  // a new scene: the competitive candidates only
             t.epoch = c->grid_epoch;
         }
@@ -1476,6 +1496,11 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
         t.chosen = b;
         t.settled = t.best[b];
         t.since = 0;
+        if (tune_log())
+            fprintf(stderr, "[vct tune] key %016llx chose %d (%.4f ms) of %d candidates; best ms %.4f %.4f %.4f %.4f; "
+                            "retime %u%s\n",
+                    (unsigned long long)t.key, b, t.best[b], n, t.best[0], t.best[1], t.best[2], t.best[3], t.retimes,
+                    t.limited ? " (competitive only)" : "");
         for (int f = 0; f < 4; ++f)              // samples still in flight belong to the timing
             for (bool& bz : t.busy[f]) bz = false;
         return t.chosen;
