@@ -317,7 +317,8 @@ uint32_t   vct_num_levels(const vct_ctx* ctx);                 /* L + 1 */
 vct_status vct_level_dims(const vct_ctx* ctx, uint32_t level, uint32_t* n_l, uint32_t* n_faces);
 /* level 0: face must be 0; host_rgba receives n_l^3 x 4 floats */
 vct_status vct_download_level(vct_ctx* ctx, uint32_t level, uint32_t face, float* host_rgba);
-/* replaces the level-0 radiance grid (n^3 x 4 floats, host) */
+/* replaces the level-0 radiance grid (n^3 x 4 floats, host); every value must be finite
+ * (VCT_EINVAL otherwise: K4's branch-free compositing needs finite samples) */
 vct_status vct_upload_level0(vct_ctx* ctx, const float* host_rgba);
 /* device pointer + size of the level-0 radiance grid (RCCL broadcast buffer).
  * Device-side level 0 is in the library's internal texel layout (2x2x2 bricks of
@@ -329,7 +330,7 @@ vct_status vct_level0_device(vct_ctx* ctx, void** dptr, size_t* bytes);
 /* device-to-device copies of the level-0 grid on the ctx stream (host RCCL
  * glue that owns its own communication buffer, e.g. a torch tensor) */
 vct_status vct_copy_level0_to_device(vct_ctx* ctx, void* dst);
-vct_status vct_set_level0_from_device(vct_ctx* ctx, const void* src);
+vct_status vct_set_level0_from_device(vct_ctx* ctx, const void* src);   /* finite values (not checked) */
 /* K1 outputs: resolved albedo/occupancy and normal grids (n^3 x 4 floats each) */
 vct_status vct_download_voxels(vct_ctx* ctx, float* albedo_occ4, float* normal4);
 /* K1 raw accumulators: sums6 [n^3][6] int64 (albedo rgb, normal xyz; 16.16 fixed

@@ -626,6 +626,8 @@ vct_status vct_download_level(vct_ctx* c, uint32_t level, uint32_t face, float* 
 
 vct_status vct_upload_level0(vct_ctx* c, const float* host) {
     if (!c || !host) return VCT_EINVAL;
+    for (size_t i = 0; i < (size_t)c->n * c->n * c->n * 4; ++i)
+        if (!isfinite(host[i])) return fail(c, VCT_EINVAL, "upload_level0: non-finite value");
     memcpy(c->r0, host, (size_t)c->n * c->n * c->n * 16);
     c->injected = 1;
     c->mipped = 0;

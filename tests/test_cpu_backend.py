@@ -299,3 +299,19 @@ def test_comm_one_rank(cpu_lib):
     ref = ctx.trace(*gb, cam.position)
     assert np.array_equal(d, ref["diffuse"]) and np.array_equal(sp, ref["spec"])
     ctx.comm_destroy()
+
+
+def test_upload_level0_refuses_non_finite(cpu_lib):
+    """K4 composites branch-free (a finished lane adds fmaf(+0, sample, c)), which needs
+    finite radiance: vct_upload_level0 refuses Inf / NaN (both libraries check it on the
+    host, before any device work)."""
+    from vct import Context, VctError
+    ctx = Context(8, (0, 0, 0), 1.0, lib=cpu_lib)
+    r0 = np.zeros((8, 8, 8, 4), np.float32)
+    ctx.upload_level0(r0)
+    for bad in (np.inf, -np.inf, np.nan):
+        r = r0.copy()
+        r[3, 4, 5, 1] = bad
+        with pytest.raises(VctError, match="EINVAL"):
+            ctx.upload_level0(r)
+    ctx.close()

@@ -778,9 +778,14 @@ vct_status vct_download_level(vct_ctx* c, uint32_t level, uint32_t face, float* 
 
 vct_status vct_upload_level0(vct_ctx* c, const float* host) {
     if (!c || !host) return VCT_EINVAL;
+    const size_t nv = (size_t)c->grid.n * c->grid.n * c->grid.n;
+    // K4 relies on finite radiance (a terminated lane's fmaf(+0, sample, c) must leave c):
+    // refuse Inf / NaN here rather than let them reach other lanes' outputs
+    for (size_t i = 0; i < nv * 4; ++i)
+        if (!std::isfinite(host[i]))
+            return fail(c, VCT_EINVAL, "upload_level0: non-finite value at float " + std::to_string(i));
     vct_status st = use_device(c);
     if (st != VCT_OK) return st;
-    const size_t nv = (size_t)c->grid.n * c->grid.n * c->grid.n;
     void* tmp;
     VCT_HIP(scratch_get(c, 0, nv * 16, &tmp), "scratch");
     VCT_HIP(hipMemcpyAsync(tmp, host, nv * 16, hipMemcpyHostToDevice, c->stream), "upload level0");

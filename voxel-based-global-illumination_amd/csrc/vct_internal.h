@@ -72,13 +72,14 @@ struct Scratch {
 // fastest.  After that the launch path never blocks: every kWatchEvery-th launch of the
 // chosen candidate is timed with an event pair polled by hipEventQuery.  The entry times
 // its candidates again only when (a) kDriftRuns consecutive samples run more than kDrift
-// times the settled time (the G-buffer or the scene changed what is fastest: every
-// candidate is timed), or (b) a new voxelization (scene) has happened and the entry has
-// run kEpochMin launches since its last timing: then only the candidates within
-// kCompetitive of the previous winner are timed, so a candidate known to be much slower
-// (screen order on an incoherent G-buffer: 6x) never runs in steady state.  A re-timing
-// keeps the first sample of each candidate (its code is loaded already) and drops a
-// candidate after one sample that is kCompetitive times slower than the best so far.
+// times the settled time (the G-buffer or the scene changed what is fastest), or (b) a
+// new voxelization (scene) has happened and the entry has run `epoch_wait` launches
+// since its last timing; epoch_wait starts at kEpochMin and doubles (up to kEpochMax)
+// each time such a re-timing keeps the same winner, so a host that re-voxelizes every
+// frame re-times rarely once the choice is stable.  A re-timing keeps the first sample
+// of each candidate (its code is loaded already) and drops a candidate after one sample
+// that is kCompetitive times slower than the best so far: a much slower candidate
+// (screen order on an incoherent G-buffer: 6x) costs one frame per re-timing.
 // VCT_TUNE_LOG=1 prints every decision to stderr.
 struct K4Tuner {
     static constexpr int kSlots = 4;          // event pairs in flight per candidate
@@ -87,7 +88,7 @@ struct K4Tuner {
     static constexpr uint32_t kWatchEvery = 2;
     static constexpr int kDriftRuns = 3;
     static constexpr float kDrift = 1.35f;
-    static constexpr uint32_t kEpochMin = 16;
+    static constexpr uint32_t kEpochMin = 16, kEpochMax = 4096;
     static constexpr float kCompetitive = 1.5f;
     struct Entry {
         uint64_t key = ~0ull;                 // workload the entry belongs to
@@ -99,8 +100,9 @@ struct K4Tuner {
         uint32_t launches = 0;                // timed launches while choosing
         uint32_t retimes = 0;                 // re-timings after the first choice
         uint32_t epoch = 0;                   // vct_ctx::grid_epoch the choice was made on
-        bool limited = false;                 // this timing skips the candidates in `skip`
-        bool skip[4] = {false, false, false, false};
+        uint32_t epoch_wait = kEpochMin;      // launches before a new scene re-times the entry
+        int prev = -1;                        // the winner before this timing (-1: none)
+        bool by_epoch = false;                // this timing was started by a new scene
         hipEvent_t ev[4][kSlots][2] = {};
         bool busy[4][kSlots] = {};
         int head[4] = {0, 0, 0, 0};

@@ -259,13 +259,19 @@ __global__ void __launch_bounds__(kTailB * kTailB * kTailB) k3_tail(const TailK 
         float4* tmp = cin; cin = cout; cout = tmp;
     }
     if (l == k.L) return;                                    // one block per face reached the top
-    // the last block of face f builds the levels above the subtree tops
-    __threadfence();                                         // release this block's writes
-    if (t == 0) s_ticket = atomicAdd(&k.tickets[f], 1u);
+    // the last block of face f builds the levels above the subtree tops.  One lane fences
+    // and takes the ticket: a device-scope fence writes back / invalidates the XCD's L2, so
+    // every wave doing its own would serialize thousands of them
+    __syncthreads();                                         // every wave's stores have been issued
+    if (t == 0) {
+        __threadfence();                                     // release the block's writes
+        s_ticket = atomicAdd(&k.tickets[f], 1u);
+    }
     __syncthreads();
     const uint32_t nblocks = nbx * nbx * nbx;
     if (s_ticket != nblocks - 1u) return;
-    __threadfence();                                         // acquire the other blocks' writes
+    if (t == 0) __threadfence();                             // acquire the other blocks' writes
+    __syncthreads();
     const uint32_t nt = nbx;                                 // subtree tops per axis (level l)
     if ((uint32_t)t < nt * nt * nt) {
         const uint32_t x = t % nt, y = (t / nt) % nt, z = t / (nt * nt);

@@ -1384,16 +1384,14 @@ static bool tune_log() {
     return on;
 }
 
-static void k4_retime(K4Tuner::Entry& t, bool limited) {
-    // limited: keep only the candidates within kCompetitive of the previous winner
+static void k4_retime(K4Tuner::Entry& t, bool by_epoch) {
     for (int f = 0; f < 4; ++f) {
-        t.skip[f] = limited && t.chosen >= 0 && t.seen[f] > K4Tuner::kSamples &&
-                    t.best[f] > K4Tuner::kCompetitive * t.best[t.chosen];
         t.seen[f] = 1;                           // warm code: no cold sample to drop
         t.best[f] = 0.0f;
         for (bool& b : t.busy[f]) b = false;     // watch samples in flight: not timing samples
     }
-    t.limited = limited;
+    t.prev = t.chosen;
+    t.by_epoch = by_epoch;
     t.chosen = -1;
     t.drift = 0;
     t.since = t.launches = 0;
@@ -1418,6 +1416,7 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
         for (int f = 0; f < 4; ++f) e.seen[f] = 0;   // first timing: drop each candidate's cold sample
         e.retimes = 0;
         e.epoch = c->grid_epoch;
+        e.epoch_wait = K4Tuner::kEpochMin;
     }
     K4Tuner::Entry& t = T.e[ix];
     t.used = ++T.clock;
@@ -1459,23 +1458,16 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
                         (unsigned long long)t.key, t.chosen, t.settled);
             k4_retime(t, false);                 // the workload changed under the key: every candidate
             t.epoch = c->grid_epoch;
-        } else if (t.epoch != c->grid_epoch && t.since >= K4Tuner::kEpochMin) {
-            if (tune_log()) fprintf(stderr, "[vct tune] key %016llx: new scene: time again\n", (unsigned long long)t.key);
-            k4_retime(t, true);                  // a new scene: the competitive candidates only
+        } else if (t.epoch != c->grid_epoch && t.since >= t.epoch_wait) {
+            if (tune_log())
+                fprintf(stderr, "[vct tune] key %016llx: new scene (after %u launches): time again\n",
+                        (unsigned long long)t.key, t.since);
+            k4_retime(t, true);
             t.epoch = c->grid_epoch;
         }
     }
-    // the candidates of this timing
-    int cands[4], n = 0;
-    for (int i = 0; i < n_in; ++i)
-        if (!(t.limited && t.skip[cands_in[i]])) cands[n++] = cands_in[i];
-    if (n == 0) cands[n++] = cands_in[0];
-    if (t.chosen < 0 && n == 1) {                // one competitive candidate left: nothing to time
-        t.chosen = cands[0];
-        t.settled = 0.0f;
-        t.since = 0;
-        return t.chosen;
-    }
+    const int* cands = cands_in;
+    const int n = n_in;
     if (t.chosen >= 0) {
         if (!timed || ++t.since % K4Tuner::kWatchEvery != 0) return t.chosen;
         const int f = t.chosen, sl = t.head[f];
@@ -1496,11 +1488,14 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
         t.chosen = b;
         t.settled = t.best[b];
         t.since = 0;
+        if (t.by_epoch)                          // a scene change that kept the winner: wait longer next time
+            t.epoch_wait = b == t.prev ? (t.epoch_wait * 2u > K4Tuner::kEpochMax ? K4Tuner::kEpochMax : t.epoch_wait * 2u)
+                                       : K4Tuner::kEpochMin;
         if (tune_log())
             fprintf(stderr, "[vct tune] key %016llx chose %d (%.4f ms) of %d candidates; best ms %.4f %.4f %.4f %.4f; "
                             "retime %u%s\n",
                     (unsigned long long)t.key, b, t.best[b], n, t.best[0], t.best[1], t.best[2], t.best[3], t.retimes,
-                    t.limited ? " (competitive only)" : "");
+                    t.by_epoch ? " (new scene)" : "");
         for (int f = 0; f < 4; ++f)              // samples still in flight belong to the timing
             for (bool& bz : t.busy[f]) bz = false;
         return t.chosen;
