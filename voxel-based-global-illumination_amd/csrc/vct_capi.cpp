@@ -74,6 +74,44 @@ hipError_t scratch_get(vct_ctx* c, int i, size_t bytes, void** out) {
     *out = s.p;
     return hipSuccess;
 }
+
+hipError_t k4_scratch(vct_ctx* c, int i, size_t bytes, void** out, bool* fresh) {
+    StreamScratch* set = nullptr;
+    for (StreamScratch& e : c->k4s)
+        if (e.used && e.s == c->stream) set = &e;
+    if (!set)
+        for (StreamScratch& e : c->k4s)
+            if (!e.used) { set = &e; break; }
+    if (!set) {   // a fifth stream: release every set (the device finishes what used them)
+        hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) return e;
+        for (StreamScratch& ss : c->k4s) {
+            for (Scratch& sc : ss.sc)
+                if (sc.p) (void)hipFree(sc.p);
+            ss = StreamScratch{};
+        }
+        set = &c->k4s[0];
+    }
+    set->used = true;
+    set->s = c->stream;
+    Scratch& sc = set->sc[i];
+    if (fresh) *fresh = false;
+    if (sc.bytes < bytes) {
+        if (sc.p) {
+            hipError_t e = hipStreamSynchronize(c->stream);   // only this stream used the set
+            if (e != hipSuccess) return e;
+            (void)hipFree(sc.p);
+            sc.p = nullptr;
+            sc.bytes = 0;
+        }
+        hipError_t e = hipMalloc(&sc.p, bytes);
+        if (e != hipSuccess) return e;
+        sc.bytes = bytes;
+        if (fresh) *fresh = true;
+    }
+    *out = sc.p;
+    return hipSuccess;
+}
 }  // namespace vct
 
 extern "C" {
@@ -236,6 +274,9 @@ void vct_destroy(vct_ctx* c) {
     if (c->spec_rows) (void)hipFree(c->spec_rows);
     for (auto& s : c->scratch)
         if (s.p) (void)hipFree(s.p);
+    for (auto& ss : c->k4s)
+        for (auto& s : ss.sc)
+            if (s.p) (void)hipFree(s.p);
     if (c->ev) (void)hipEventDestroy(c->ev);
     for (auto& en : c->k4tune.e)
         for (auto& f : en.ev)

@@ -56,6 +56,17 @@ struct Scratch {
     size_t bytes = 0;
 };
 
+// K4's per-launch scratch, one set per stream: K4 launches on different streams may run
+// concurrently (a host that overlaps consecutive frames), so the cone-split hand-over
+// and the ray-reorder buffers belong to the stream, not to the context.
+enum { kScFlags = 0, kScHand = 1, kScKeys = 2, kScSort = 3, kScN = 4 };
+struct StreamScratch {
+    hipStream_t s = nullptr;
+    bool used = false;
+    Scratch sc[kScN];
+};
+constexpr int kStreamSets = 4;
+
 // K4 candidate choice (vct_trace.hip k4_form).  The default cone trace has two
 // bit-identical compiled forms: the four-face-union form (4 waves/SIMD; pays on curved
 // surfaces, where a wave's lanes straddle an axis) and the occupancy form (5 waves/SIMD,
@@ -125,9 +136,9 @@ struct vct_ctx {
     vct::Mesh mesh;
     vct::Textures tex;
     vct::Scratch scratch[12];    // reusable scratch (0 trace host staging, 1 voxelize temps,
-                                  // 2-3 G-buffer bins, 4 K2 work list, 5-6 K4 cone-split hand-over,
-                                  // 7 K1 candidate bucket table, 8 multi-device tiles / gather,
-                                  // 9 multi-device step counters, 10-11 ray reorder keys / sort temps)
+                                  // 2-3 G-buffer bins, 4 K2 work list, 7 K1 candidate bucket table,
+                                  // 8 multi-device tiles / gather, 9 multi-device step counters)
+    vct::StreamScratch k4s[vct::kStreamSets];   // K4 hand-over + reorder scratch per stream (k4_scratch)
     vct::K4Tuner k4tune;                // timed-form choice of the default cone trace
     uint32_t grid_epoch = 0;            // bumped by every voxelization (a new scene for the tuner)
     vct::StepRow* step_tab = nullptr;   // [kMaxStepRows] diffuse-cone step table (device)
@@ -191,5 +202,8 @@ int build_step_table(float tau, uint32_t n, uint32_t L, StepRow* rows);
 
 // scratch helper: grows scratch slot `i` to at least `bytes`
 hipError_t scratch_get(vct_ctx* c, int i, size_t bytes, void** out);
+// K4 scratch `i` (kSc*) of the ctx's current stream, grown to at least `bytes`; *fresh: it
+// was (re)allocated by this call (contents undefined)
+hipError_t k4_scratch(vct_ctx* c, int i, size_t bytes, void** out, bool* fresh);
 
 }  // namespace vct

@@ -304,7 +304,11 @@ __global__ void __launch_bounds__(256) k_relayout(const float4* __restrict__ src
 
 hipError_t launch_mips(vct_ctx* c) {
     Grid& g = c->grid;
-    const bool old = getenv("VCT_K3_PER_LEVEL") != nullptr;   // A/B: one thread-per-parent launch per level
+    // A/B (VCT_K3_FUSED=1): thread-per-(parent, face) levels + the fused tail launch.  Measured
+    // slower than one thread-per-parent launch per level (256^3: 0.219 vs 0.170 ms; 512^3:
+    // 1.51 vs 1.17 ms, tools/k3_bench.py): the per-lane 128-B brick reads are uncoalesced
+    // either way and the face split only multiplies them; kept for the record
+    const bool old = getenv("VCT_K3_FUSED") == nullptr;
     // the small levels (<= 32^3 parents, level >= 2) go to the fused tail launch
     uint32_t ls = 2;
     while (ls <= g.L && (g.n >> ls) > 32u) ++ls;

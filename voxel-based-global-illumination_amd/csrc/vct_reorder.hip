@@ -66,8 +66,8 @@ hipError_t launch_reorder(vct_ctx* c, const vct_trace_args* a, const uint32_t** 
     if (e != hipSuccess) return e;
     void* kv = nullptr;   // [keys in | keys out | values in | values out]
     void* tmp = nullptr;
-    if ((e = scratch_get(c, 10, 4 * pairs, &kv)) != hipSuccess) return e;
-    if ((e = scratch_get(c, 11, tmp_bytes ? tmp_bytes : 1, &tmp)) != hipSuccess) return e;
+    if ((e = k4_scratch(c, kScKeys, 4 * pairs, &kv, nullptr)) != hipSuccess) return e;
+    if ((e = k4_scratch(c, kScSort, tmp_bytes ? tmp_bytes : 1, &tmp, nullptr)) != hipSuccess) return e;
     uint32_t* keys_in = (uint32_t*)kv;
     uint32_t* keys_out = keys_in + npx;
     uint32_t* vals_in = keys_out + npx;

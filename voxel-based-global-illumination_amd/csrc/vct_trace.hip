@@ -1614,13 +1614,14 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         k.ndp = (int)(((uint32_t)k.nd + chunk - 1u) / chunk);   // no empty part
         const size_t npx = k.compact ? (size_t)nlt * VCT_TILE * VCT_TILE : (size_t)a->width * a->height;
         const size_t fbytes = (size_t)blocks * 4 * sizeof(unsigned);
-        const bool fresh = c->scratch[5].bytes < fbytes;    // flags: zeroed when allocated, then
+        bool fresh = false;                                  // flags: zeroed when allocated, then
         void* fp = nullptr;                                  // reset by the kernel after each hand-over
         void* sp = nullptr;
-        hipError_t e = scratch_get(c, 5, fbytes, &fp);
+        hipError_t e = k4_scratch(c, kScFlags, fbytes, &fp, &fresh);
         if (e != hipSuccess) return e;
-        if (fresh && (e = hipMemsetAsync(fp, 0, c->scratch[5].bytes, c->stream)) != hipSuccess) return e;
-        if ((e = scratch_get(c, 6, (size_t)(1 + k.nd - k.nd_chunk) * npx * sizeof(float4), &sp)) != hipSuccess)
+        if (fresh && (e = hipMemsetAsync(fp, 0, fbytes, c->stream)) != hipSuccess) return e;
+        if ((e = k4_scratch(c, kScHand, (size_t)(1 + k.nd - k.nd_chunk) * npx * sizeof(float4), &sp, nullptr)) !=
+            hipSuccess)
             return e;
         k.split = 2;
         k.sc_flag = (unsigned*)fp;
