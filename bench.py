@@ -14,10 +14,15 @@ each rank traces its interleaved 64x64 tiles (tile t -> rank t % N) and, for
 N > 1, the frame is assembled on the presenting rank 0 (every rank sends
 exactly its own tiles over RCCL; `--exchange allgather` all-gathers to every
 rank instead) and un-permuted there (strong scaling: the frame is fixed, the
-tiles are split).  Frames are pipelined as a renderer's frame loop runs them:
-the exchange of frame f overlaps the trace of frame f+1 (vct.multi.FrameTracer);
-every timed step still traces, exchanges and un-permutes one whole frame, and
-the pipeline is drained inside the timed region.  The level-0 grid is injected
+tiles are split).  Frames are pipelined as a renderer's frame loop runs them
+(vct.multi.FrameTracer): frame f is traced on trace stream f % 2, so the next
+frame's trace fills the tail of the previous K4 launch, and the exchange of
+frame f overlaps the trace of frame f+1 (`--no-overlap`: one stream); every
+timed step still traces, exchanges and un-permutes one whole frame, and the
+pipeline is drained inside the timed region.  The roofline's K4 launch
+duration (`k4_kernel_ms_avg`) is timed after the loop with K frames back to
+back on one stream (the kernel alone); `k4_kernel_ms_avg_overlapped` is the
+launches' average inside the pipelined loop, where two traces share the chip.  The level-0 grid is injected
 on rank 0 and broadcast (RCCL) before the timed region, as when the light
 changes; every other rank also injects it itself (the replicated alternative,
 checked bit-equal); K1/K2/K3, the broadcast, the trace alone (slowest rank) and
@@ -107,6 +112,8 @@ def parse():
                    help="N = 1: frames of the steady-state hitch loop per G-buffer (0: skip)")
     p.add_argument("--multi-config", default="c4,c5",
                    help="BASELINE configs[3] / [4] measured beside the metric (comma list; empty or 'none': skip)")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="trace every frame on one stream (default: consecutive frames on two streams)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-json", default=PROFILE)
@@ -474,7 +481,8 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
         gb = tuple(torch.from_numpy(a).to(dev) for a in host)
     torch.cuda.synchronize()
 
-    tracer = FrameTracer(ctx, torch, dist, w, h, rank, world, dev, mode=args.exchange)
+    tracer = FrameTracer(ctx, torch, dist, w, h, rank, world, dev, mode=args.exchange,
+                         overlap=False if args.no_overlap else None)
     # counting pass (same kernel, counters on): frame cone steps and texel fetches
     cnt = torch.zeros(2, dtype=torch.int64, device=dev)
     steps_px = torch.zeros((h, w), dtype=torch.int32, device=dev)
@@ -501,21 +509,30 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        ev[s][0].record(stream)
-        tracer.step(gb, eye, variant=args.variant, on_traced=lambda: ev[s][1].record(stream))
+        tracer.step(gb, eye, variant=args.variant, events=ev[s])
     tracer.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(torch, dist, dev, [elapsed], world)[0]
-    k4_ms = [a.elapsed_time(b) for a, b in ev]
+    k4_ov_ms = [a.elapsed_time(b) for a, b in ev]
+    # K4 alone (the roofline's launch duration): K frames back to back on the ctx stream,
+    # no other work on the GPU -- in the pipelined loop consecutive traces share the chip
+    iev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for s in range(args.steps):
+        iev[s][0].record(stream)
+        tracer.trace_local(gb, eye, variant=args.variant)
+        iev[s][1].record(stream)
+    torch.cuda.synchronize()
+    k4_ms = [a.elapsed_time(b) for a, b in iev]
     k4_avg_ms = sum(k4_ms) / len(k4_ms)
     k4_med_ms = sorted(k4_ms)[len(k4_ms) // 2]
     ms_per_step = elapsed / args.steps * 1e3
     r.update({
         "value": frame_steps * args.steps / elapsed / 1e6, "ms_per_step": ms_per_step, "frame_cone_steps": frame_steps,
         "valid_px": frame_valid, "k4_kernel_ms_avg": k4_avg_ms, "k4_kernel_ms_median": k4_med_ms,
+        "k4_kernel_ms_avg_overlapped": sum(k4_ov_ms) / len(k4_ov_ms), "overlap": tracer.overlap,
         "local_texels": local_texels, "local_valid": local_valid,
         "frame_relight_ms": round(min(k2_ms + bcast_ms, k2_rep_ms) + k3_ms + ms_per_step, 3),
         "frame_relight_bcast_ms": round(k2_ms + bcast_ms + k3_ms + ms_per_step, 3),
@@ -813,6 +830,8 @@ def run(args, world):
             result[k_] = m[k_]
         result["k4_kernel_ms_avg"] = round(m["k4_kernel_ms_avg"], 4)
         result["k4_kernel_ms_median"] = round(m["k4_kernel_ms_median"], 4)
+        result["k4_kernel_ms_avg_overlapped"] = round(m["k4_kernel_ms_avg_overlapped"], 4)
+        result["frame_overlap"] = "two trace streams" if m["overlap"] else "one stream"
         result["k4_form"] = form_name(m["k4_form"])
         for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
                    "frame_relight_bcast_ms", "frame_relight_replicated_ms", "replicated_k2_equals_bcast",

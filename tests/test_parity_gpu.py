@@ -328,11 +328,27 @@ class _FakeGroup:
     """Stands in for an RCCL group of `world` ranks driven from ONE process: a
     rank's all_gather_into_tensor is completed when its work is waited on, from
     every rank's input of the same round (the inputs must still be intact then,
-    which is exactly what FrameTracer's double buffering promises)."""
+    which is exactly what FrameTracer's double buffering promises).  As with RCCL,
+    an op is ordered after the work queued on the stream current when it is
+    issued (an event recorded there), and a waited work orders the waiting
+    stream after the copy."""
 
     def __init__(self, world):
         self.world, self.inputs, self.round = world, {}, [0] * world
         self.sends, self.p2p_round = {}, {}
+
+    @staticmethod
+    def _issued():
+        import torch
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
+    @staticmethod
+    def _after(evs):
+        import torch
+        for ev in evs:
+            torch.cuda.current_stream().wait_event(ev)
 
     def view(self, rank):
         g = self
@@ -344,11 +360,12 @@ class _FakeGroup:
             def all_gather_into_tensor(self, out, inp, async_op=False):
                 rd = g.round[rank]
                 g.round[rank] += 1
-                g.inputs[(rd, rank)] = inp
+                g.inputs[(rd, rank)] = (inp, g._issued())
 
                 def done():
+                    g._after([g.inputs[(rd, r)][1] for r in range(g.world)])
                     for r in range(g.world):
-                        out[r].copy_(g.inputs[(rd, r)])
+                        out[r].copy_(g.inputs[(rd, r)][0])
                 if not async_op:
                     done()
                     return None
@@ -369,24 +386,29 @@ class _FakeGroup:
                     rd = g.p2p_round.get((src, dst, o.op), 0)
                     g.p2p_round[(src, dst, o.op)] = rd + 1
                     if o.op == "isend":
-                        g.sends[(rd, src, dst)] = o.tensor
+                        g.sends[(rd, src, dst)] = (o.tensor, g._issued())
                         works.append(_FakeWork(lambda: None))
                     else:
-                        works.append(_FakeWork(lambda t=o.tensor, k=(rd, src, dst): t.copy_(g.sends[k].view_as(t))))
+                        def recv(t=o.tensor, k=(rd, src, dst)):
+                            g._after([g.sends[k][1]])
+                            t.copy_(g.sends[k][0].view_as(t))
+                        works.append(_FakeWork(recv))
                 return works
         return View()
 
 
+@pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("world,mode", [(1, "present"), (2, "present"), (3, "present"), (2, "allgather"),
                                         (3, "allgather")])
-def test_frame_pipeline_equals_full_frames(gpu_ready, world, mode):
+def test_frame_pipeline_equals_full_frames(gpu_ready, world, mode, overlap):
     """FrameTracer (bench.py's per-rank driver): the pipelined step()/drain() loop
     (the exchange of frame f overlapping the trace of frame f+1, two buffer sets,
     [diffuse | specular] moved together, one two-plane untile) yields every frame
     bit-identical to a single-rank trace of it, on rank 0 only ("present": send /
     recv of each rank's own tiles, packed) or on every rank ("allgather").  Ranks
     are FrameTracers in one process over a fake group; each frame uses a different
-    eye (specular changes)."""
+    eye (specular changes).  overlap: frames traced on two streams (consecutive K4
+    launches run concurrently, each with its own hand-over / reorder scratch)."""
     import torch
     from vct import scenes
     from vct.camera import Camera
@@ -405,12 +427,13 @@ def test_frame_pipeline_equals_full_frames(gpu_ready, world, mode):
         ctx.trace_device(pos, nrm, alb, w, h, e, d, sp)
         refs.append((d, sp))
     grp = _FakeGroup(world)
-    tr = [FrameTracer(ctx, torch, grp.view(r), w, h, r, world, dev, mode=mode) for r in range(world)]
+    tr = [FrameTracer(ctx, torch, grp.view(r), w, h, r, world, dev, mode=mode, overlap=overlap)
+          for r in range(world)]
     for f, e in enumerate(eyes):
         for t in tr:
             t.step((pos, nrm, alb), e)
-        # one rank: the frame is done; several: frame f-1 was completed inside step(f)
-        done = f if world == 1 else f - 1
+        # one rank without overlap: the frame is done; else frame f-1 was completed inside step(f)
+        done = f if (world == 1 and not overlap) else f - 1
         if done >= 0:
             torch.cuda.synchronize()
             for t in tr:

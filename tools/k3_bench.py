@@ -1,6 +1,6 @@
 """K3 (mip build) timing on one GPU: the atrium at n^3, build_mips `reps` times; run under
-rocprofv3 --kernel-trace --stats for the per-kernel split (VCT_K3_FUSED=1: the
-per-(parent, face) levels + one fused tail launch, for A/B)."""
+rocprofv3 --kernel-trace --stats for the per-kernel split (VCT_K3_PLAN=level: one
+lane-per-parent launch per level, for A/B against the block-subtree plan)."""
 import argparse
 import os
 import sys
@@ -32,7 +32,7 @@ def main():
     e1.record(st)
     torch.cuda.synchronize()
     print(f"n={a.n} K3 {e0.elapsed_time(e1) / a.reps:.4f} ms per build "
-          f"({'fused tail' if os.environ.get('VCT_K3_FUSED') else 'per-level'})")
+          f"({'per-level' if os.environ.get('VCT_K3_PLAN') == 'level' else 'block subtrees'})")
 
 
 if __name__ == "__main__":

@@ -264,7 +264,6 @@ void vct_destroy(vct_ctx* c) {
     if (g.occ_count) (void)hipFree(g.occ_count);
     if (g.accum) (void)hipFree(g.accum);
     if (c->k1_err) (void)hipFree(c->k1_err);
-    if (c->k3_tickets) (void)hipFree(c->k3_tickets);
     if (c->mesh.tri) (void)hipFree(c->mesh.tri);
     if (c->mesh.uv) (void)hipFree(c->mesh.uv);
     if (c->tex.texels) (void)hipFree(c->tex.texels);

@@ -145,7 +145,6 @@ struct vct_ctx {
     unsigned* spec_keys = nullptr;      // [2 * kSpecSlots]: specular table keys (~0u free), then states
     vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)
     int* k1_err = nullptr;              // device flag of vct_voxelize_device (index out of range)
-    unsigned* k3_tickets = nullptr;     // [6] K3 tail: per-face workgroup tickets (0 between builds)
     // vct_create_multi: this context is device rank 0 and owns one context per
     // further device (ranks 1..n-1); empty for a single-device context
     std::vector<vct_ctx*> peers;

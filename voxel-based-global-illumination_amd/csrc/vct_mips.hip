@@ -5,23 +5,24 @@
 // (c = f + (1 - f.a) * b) and averaged.  Level 1 reads the isotropic level-0
 // radiance grid; level l >= 2 reads the same face of level l-1.
 //
-// MI355X design: the pyramid is pure HBM streaming (reads 8 texels and writes
-// 1 per face).  In the brick layout (vct_device.h VCT_BRICK2) a parent's eight
-// children are one 128-byte brick: every read is a whole cache line.  At 256^3 the
-// pyramid moves ~0.7 GB, 0.46 GB of it in level 1.
-//  * level 1 (k3_level1): one thread per parent texel reads its eight isotropic
-//    children once and writes all six faces;
-//  * levels >= 2 with more than 32^3 parents (k3_levelN_face): one thread per
-//    (parent texel, face), one 128-B brick in, one texel out -- six times the
-//    threads of a thread-per-parent kernel, so the loads of a level are in flight
-//    together instead of six dependent rounds;
-//  * the small levels (<= 32^3 parents; 6 of the 8 levels at 256^3) in ONE launch
-//    (k3_tail): a workgroup builds an 8^3-parent subtree of one face level by level
-//    in LDS, and the last workgroup of each face (an atomic ticket) finishes the
-//    levels above the subtrees.  Those levels were one launch each, 4-6 us apiece
-//    for a few MB.
+// MI355X design: the pyramid is pure HBM streaming.  In the brick layout (vct_device.h
+// VCT_BRICK2) a parent's eight children are one 128-byte brick, and the bricks of a row of
+// parents are contiguous.  k3_block: a workgroup owns an E^3 block of parents of level l
+// (E = min(8, n_l)) and builds their whole subtree, levels l .. l + log2 E, in LDS:
+//  * its 512 child bricks are staged through LDS with coalesced loads (a wave-instruction
+//    reads 1 KB contiguous: eight bricks of a row), so every load instruction touches 8
+//    cache lines instead of the 64 of a lane-per-parent brick read (the per-level
+//    kernels below ran level 1 at 5.2 TB/s and level 2 at 4.3 TB/s that way);
+//  * levels l+1 .. l+log2 E come from LDS, so only level 0 and the subtree tops are ever
+//    read from HBM: at 256^3 one launch reads level 0 (268 MB) and writes levels 1-4 of
+//    all six faces (230 MB); a second one (6 workgroups) builds levels 5-8.  The
+//    per-level plan read every level back (695 MB) in 8 launches.
+// Level 1 of an anisotropic pyramid takes the isotropic level 0 and writes all six faces
+// (each thread: one parent, six faces); levels >= 2 read the same face (blockIdx.y).
+// VCT_K3_PLAN=level selects the per-level kernels (one launch per level) for A/B.
 // Every texel is computed with the same operations in the same order as the oracle.
 #include <cstdlib>
+#include <cstring>
 
 #include "vct_internal.h"
 
@@ -99,6 +100,19 @@ __device__ __forceinline__ float4 face_of(const float4 (&ch)[2][2][2], int f) {
             acc = add4(acc, comp(tf, tb));
         }
     return scale4(acc, 0.25f);
+}
+
+// face_of for a face known only at run time: one constant-index body per face (a
+// run-time index into ch would put the children in scratch)
+__device__ __forceinline__ float4 face_rt(const float4 (&ch)[2][2][2], int f) {
+    switch (f) {
+        case 0: return face_of(ch, 0);
+        case 1: return face_of(ch, 1);
+        case 2: return face_of(ch, 2);
+        case 3: return face_of(ch, 3);
+        case 4: return face_of(ch, 4);
+        default: return face_of(ch, 5);
+    }
 }
 
 __device__ __forceinline__ float4 box_of(const float4 (&ch)[2][2][2]) {
@@ -179,113 +193,102 @@ __global__ void __launch_bounds__(256) k3_levelN(const float4* __restrict__ src,
     }
 }
 
-// level l >= 2, one thread per (parent texel v, face blockIdx.y); aniso = 0: one face, box filter
-__global__ void __launch_bounds__(256) k3_levelN_face(const float4* __restrict__ src, float4* __restrict__ dst,
-                                                      int nl, int aniso) {
-    const size_t vl = (size_t)nl * nl * nl;
-    const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= vl) return;
-    const int f = (int)blockIdx.y;
-    uint32_t x, y, z;
-    texel_coords((uint32_t)v, (uint32_t)nl, x, y, z);
-    const uint32_t nc = 2u * (uint32_t)nl;
-    const size_t vc = (size_t)nc * nc * nc;
-    float4 ch[2][2][2];
-    load_children(src + (size_t)f * vc, x, y, z, nc, ch);
-    dst[(size_t)f * vl + v] = aniso ? face_of(ch, f) : box_of(ch);
-}
+// The subtree of an E^3 block of parents of level l (blockIdx.x = block, blockIdx.y = face
+// for MODE kFace).  LDS: the staged child bricks (brick c at slots 9c .. 9c + 7: a
+// ds_read_b128 lane group of 16 consecutive parents hits 16 distinct bank quads), then,
+// in the same array, each level's results (linear, x fastest) for the next one.
+enum { kIso6 = 0, kFace = 1, kBox = 2 };
+constexpr int kBlk = 8;                       // block edge (parents of level l)
+constexpr int kBlkT = kBlk * kBlk * kBlk;     // threads of a workgroup
 
-// The small levels ls..L in one launch.  Workgroup (b, f): the B^3 parents of level ls
-// in block b of face f (B = min(8, n_ls)), then their subtree up to level ls + log2 B in
-// LDS; each level is also written to the pyramid.  The last workgroup of face f to
-// finish (ticket == blocks - 1, after a device-scope fence) reads the subtree tops of
-// every block of the face and builds the levels above them the same way.
-struct TailK {
+struct BlockK {
     float4* pyr;
-    uint64_t off[kMaxLevels + 1];   // float4 offset of each level
-    int n, ls, L, aniso, B, lgB;
-    unsigned* tickets;              // [6] per face, left at 0
+    uint64_t off[kMaxLevels + 1];             // float4 offset of each level
+    int n, l;                                 // grid edge, first level built
 };
 
-constexpr int kTailB = 8;
-
-// level `l` (edge nl) of face f from the LDS children cin (edge 2E, linear) into cout
-// (edge E, linear) and the pyramid; block origin (ox, oy, oz) in level-l texels
-__device__ __forceinline__ void tail_level(const TailK& k, const float4* cin, float4* cout, int E, int l,
-                                           uint32_t ox, uint32_t oy, uint32_t oz, int f) {
+template <int MODE>
+__global__ void __launch_bounds__(kBlkT) k3_block(const BlockK k) {
+    __shared__ float4 st[kBlkT * 9];
+    constexpr int FACES = MODE == kIso6 ? 6 : 1;
     const int t = (int)threadIdx.x;
-    if (t < E * E * E) {
-        const int lx = t % E, ly = (t / E) % E, lz = t / (E * E), C = 2 * E;
+    const int f0 = MODE == kFace ? (int)blockIdx.y : 0;
+    const uint32_t nl = (uint32_t)k.n >> k.l, nc = 2u * nl;
+    const int E = nl < (uint32_t)kBlk ? (int)nl : kBlk, E3 = E * E * E;
+    const uint32_t nbk = nl / (uint32_t)E, b = blockIdx.x;
+    const uint32_t X0 = (b % nbk) * E, Y0 = ((b / nbk) % nbk) * E, Z0 = (b / (nbk * nbk)) * E;
+    // children: face f0 of level l-1 (level 0 for kIso6 and level 1 of kBox)
+    const float4* src = k.pyr + k.off[k.l - 1] + (MODE == kFace ? (size_t)f0 * nc * nc * nc : 0);
+    // staging: float4 u = 8 c + j of the block's child bricks (c linear over the block's
+    // parents, x fastest; the child brick of parent (x, y, z) is brick x + nl (y + nl z))
+    {
+        // (u < E3 * 8 always holds for E = 8; a smaller block clamps its spare loads)
+        float4 r[8];
+        const int lim = E3 * 8 - 1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int u = min(i * kBlkT + t, lim);
+            const int c = u >> 3, j = u & 7;
+            const uint32_t cx = (uint32_t)(c % E), cy = (uint32_t)((c / E) % E), cz = (uint32_t)(c / (E * E));
+            const size_t brick = (size_t)(X0 + cx) + (size_t)nl * ((size_t)(Y0 + cy) + (size_t)nl * (Z0 + cz));
+            r[i] = src[brick * 8 + j];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int u = i * kBlkT + t;
+            if (u <= lim) st[(u >> 3) * 9 + (u & 7)] = r[i];
+        }
+    }
+    __syncthreads();
+    // level l: thread t = parent t of the block
+    float4 out[FACES];
+    if (t < E3) {
         float4 ch[2][2][2];
 #pragma unroll
-        for (int dz = 0; dz < 2; ++dz)
+        for (int j = 0; j < 8; ++j) ch[j >> 2][(j >> 1) & 1][j & 1] = st[t * 9 + j];
+        if constexpr (MODE == kIso6) aniso_faces(ch, out);
+        else if constexpr (MODE == kFace) out[0] = face_rt(ch, f0);
+        else out[0] = box_of(ch);
+    }
+    __syncthreads();                          // every staged brick has been read
+    if (t < E3) {
+        const uint32_t x = X0 + (uint32_t)(t % E), y = Y0 + (uint32_t)((t / E) % E), z = Z0 + (uint32_t)(t / (E * E));
+        const size_t vl = (size_t)nl * nl * nl, ti = texel_index(x, y, z, nl);
 #pragma unroll
-            for (int dy = 0; dy < 2; ++dy)
+        for (int f = 0; f < FACES; ++f) {
+            st[f * E3 + t] = out[f];
+            k.pyr[k.off[k.l] + (size_t)(f0 + f) * vl + ti] = out[f];
+        }
+    }
+    __syncthreads();
+    // levels l+1 ..: from the previous level's results in LDS (face-major, linear)
+    int base = 0, Ein = E, l = k.l;
+    for (int Eo = E >> 1; Eo >= 1; Eo >>= 1) {
+        ++l;
+        const int cnt = Eo * Eo * Eo, nb = base + FACES * Ein * Ein * Ein;
+        const uint32_t no = (uint32_t)k.n >> l;
+        if (t < FACES * cnt) {
+            const int f = t / cnt, q = t % cnt;
+            const int qx = q % Eo, qy = (q / Eo) % Eo, qz = q / (Eo * Eo);
+            const float4* cin = st + base + f * Ein * Ein * Ein;
+            float4 ch[2][2][2];
 #pragma unroll
-                for (int dx = 0; dx < 2; ++dx)
-                    ch[dz][dy][dx] = cin[(2 * lx + dx) + C * ((2 * ly + dy) + C * (2 * lz + dz))];
-        const float4 r = k.aniso ? face_of(ch, f) : box_of(ch);
-        cout[t] = r;
-        const uint32_t nl = (uint32_t)k.n >> l;
-        k.pyr[k.off[l] + (size_t)f * nl * nl * nl + texel_index(ox + lx, oy + ly, oz + lz, nl)] = r;
+            for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+                for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 2; ++dx)
+                        ch[dz][dy][dx] = cin[(2 * qx + dx) + Ein * ((2 * qy + dy) + Ein * (2 * qz + dz))];
+            const float4 r = MODE == kBox ? box_of(ch) : face_rt(ch, f0 + f);
+            st[nb + t] = r;
+            const uint32_t ox = X0 >> (l - k.l), oy = Y0 >> (l - k.l), oz = Z0 >> (l - k.l);
+            k.pyr[k.off[l] + (size_t)(f0 + f) * no * no * no +
+                  texel_index(ox + (uint32_t)qx, oy + (uint32_t)qy, oz + (uint32_t)qz, no)] = r;
+        }
+        __syncthreads();
+        base = nb;
+        Ein = Eo;
     }
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(kTailB * kTailB * kTailB) k3_tail(const TailK k) {
-    __shared__ float4 sa[kTailB * kTailB * kTailB], sb[kTailB * kTailB * kTailB];
-    __shared__ unsigned s_ticket;
-    const int f = (int)blockIdx.y, t = (int)threadIdx.x;
-    const uint32_t ns = (uint32_t)k.n >> k.ls;              // parents per axis at level ls
-    const uint32_t nbx = ns / (uint32_t)k.B;                 // blocks per axis
-    const uint32_t b = blockIdx.x;
-    const uint32_t bx = b % nbx, by = (b / nbx) % nbx, bz = b / (nbx * nbx);
-    // level ls from level ls - 1 in the pyramid (one brick per parent)
-    if (t < k.B * k.B * k.B) {
-        const int lx = t % k.B, ly = (t / k.B) % k.B, lz = t / (k.B * k.B);
-        const uint32_t x = bx * k.B + lx, y = by * k.B + ly, z = bz * k.B + lz, nc = 2u * ns;
-        float4 ch[2][2][2];
-        load_children(k.pyr + k.off[k.ls - 1] + (size_t)f * nc * nc * nc, x, y, z, nc, ch);
-        const float4 r = k.aniso ? face_of(ch, f) : box_of(ch);
-        sa[t] = r;
-        k.pyr[k.off[k.ls] + (size_t)f * ns * ns * ns + texel_index(x, y, z, ns)] = r;
-    }
-    __syncthreads();
-    float4 *cin = sa, *cout = sb;
-    int l = k.ls;
-    for (int E = k.B >> 1; E >= 1; E >>= 1) {               // the block's subtree (edge E at level l)
-        ++l;
-        tail_level(k, cin, cout, E, l, bx * (uint32_t)E, by * (uint32_t)E, bz * (uint32_t)E, f);
-        float4* tmp = cin; cin = cout; cout = tmp;
-    }
-    if (l == k.L) return;                                    // one block per face reached the top
-    // the last block of face f builds the levels above the subtree tops.  One lane fences
-    // and takes the ticket: a device-scope fence writes back / invalidates the XCD's L2, so
-    // every wave doing its own would serialize thousands of them
-    __syncthreads();                                         // every wave's stores have been issued
-    if (t == 0) {
-        __threadfence();                                     // release the block's writes
-        s_ticket = atomicAdd(&k.tickets[f], 1u);
-    }
-    __syncthreads();
-    const uint32_t nblocks = nbx * nbx * nbx;
-    if (s_ticket != nblocks - 1u) return;
-    if (t == 0) __threadfence();                             // acquire the other blocks' writes
-    __syncthreads();
-    const uint32_t nt = nbx;                                 // subtree tops per axis (level l)
-    if ((uint32_t)t < nt * nt * nt) {
-        const uint32_t x = t % nt, y = (t / nt) % nt, z = t / (nt * nt);
-        sa[t] = k.pyr[k.off[l] + (size_t)f * nt * nt * nt + texel_index(x, y, z, nt)];
-    }
-    __syncthreads();
-    cin = sa;
-    cout = sb;
-    for (int E = (int)nt >> 1; E >= 1; E >>= 1) {
-        ++l;
-        tail_level(k, cin, cout, E, l, 0u, 0u, 0u, f);
-        float4* tmp = cin; cin = cout; cout = tmp;
-    }
-    if (t == 0) k.tickets[f] = 0u;                           // ready for the next build
 }
 
 // one face volume between the pyramid's layout and linear-Z (download / upload)
@@ -304,48 +307,36 @@ __global__ void __launch_bounds__(256) k_relayout(const float4* __restrict__ src
 
 hipError_t launch_mips(vct_ctx* c) {
     Grid& g = c->grid;
-    // A/B (VCT_K3_FUSED=1): thread-per-(parent, face) levels + the fused tail launch.  Measured
-    // slower than one thread-per-parent launch per level (256^3: 0.219 vs 0.170 ms; 512^3:
-    // 1.51 vs 1.17 ms, tools/k3_bench.py): the per-lane 128-B brick reads are uncoalesced
-    // either way and the face split only multiplies them; kept for the record
-    const bool old = getenv("VCT_K3_FUSED") == nullptr;
-    // the small levels (<= 32^3 parents, level >= 2) go to the fused tail launch
-    uint32_t ls = 2;
-    while (ls <= g.L && (g.n >> ls) > 32u) ++ls;
-    for (uint32_t l = 1; l <= g.L && (old || l < ls); ++l) {
-        const int nl = (int)(g.n >> l);
-        const size_t vl = (size_t)nl * nl * nl;
-        const uint32_t blocks = (uint32_t)((vl + 255) / 256);
-        float4* dst = g.pyr + g.lvl_off[l];
-        const float4* src = g.pyr + g.lvl_off[l - 1];
-        if (l == 1)
-            hipLaunchKernelGGL(k3_level1, dim3(blocks), dim3(256), 0, c->stream, src, dst, nl, g.aniso);
-        else if (old)
-            hipLaunchKernelGGL(k3_levelN, dim3(blocks), dim3(256), 0, c->stream, src, dst, nl, g.aniso);
-        else
-            hipLaunchKernelGGL(k3_levelN_face, dim3(blocks, g.aniso ? 6 : 1), dim3(256), 0, c->stream, src, dst, nl,
-                               g.aniso);
-    }
-    if (!old && ls <= g.L) {
-        if (!c->k3_tickets) {
-            hipError_t e = hipMalloc((void**)&c->k3_tickets, 64);
-            if (e == hipSuccess) e = hipMemsetAsync(c->k3_tickets, 0, 64, c->stream);
-            if (e != hipSuccess) return e;
+    const char* plan = getenv("VCT_K3_PLAN");
+    if (plan && strcmp(plan, "level") == 0) {    // A/B: one lane-per-parent launch per level
+        for (uint32_t l = 1; l <= g.L; ++l) {
+            const int nl = (int)(g.n >> l);
+            const size_t vl = (size_t)nl * nl * nl;
+            const uint32_t blocks = (uint32_t)((vl + 255) / 256);
+            float4* dst = g.pyr + g.lvl_off[l];
+            const float4* src = g.pyr + g.lvl_off[l - 1];
+            if (l == 1)
+                hipLaunchKernelGGL(k3_level1, dim3(blocks), dim3(256), 0, c->stream, src, dst, nl, g.aniso);
+            else
+                hipLaunchKernelGGL(k3_levelN, dim3(blocks), dim3(256), 0, c->stream, src, dst, nl, g.aniso);
         }
-        TailK k;
-        k.pyr = g.pyr;
-        for (int i = 0; i <= kMaxLevels; ++i) k.off[i] = g.lvl_off[i];
-        k.n = (int)g.n;
-        k.ls = (int)ls;
-        k.L = (int)g.L;
-        k.aniso = g.aniso;
-        const uint32_t ns = g.n >> ls;
-        k.B = (int)(ns < (uint32_t)kTailB ? ns : (uint32_t)kTailB);
-        k.lgB = __builtin_ctz((unsigned)k.B);
-        k.tickets = c->k3_tickets;
-        const uint32_t nbx = ns / (uint32_t)k.B;
-        hipLaunchKernelGGL(k3_tail, dim3(nbx * nbx * nbx, g.aniso ? 6 : 1), dim3(kTailB * kTailB * kTailB), 0,
-                           c->stream, k);
+        return hipGetLastError();
+    }
+    BlockK k;
+    k.pyr = g.pyr;
+    for (int i = 0; i <= kMaxLevels; ++i) k.off[i] = g.lvl_off[i];
+    k.n = (int)g.n;
+    for (uint32_t l = 1; l <= g.L;) {
+        const uint32_t nl = g.n >> l, E = nl < (uint32_t)kBlk ? nl : (uint32_t)kBlk;
+        const uint32_t nbk = nl / E, blocks = nbk * nbk * nbk;
+        k.l = (int)l;
+        if (!g.aniso)
+            hipLaunchKernelGGL(k3_block<kBox>, dim3(blocks), dim3(kBlkT), 0, c->stream, k);
+        else if (l == 1)
+            hipLaunchKernelGGL(k3_block<kIso6>, dim3(blocks), dim3(kBlkT), 0, c->stream, k);
+        else
+            hipLaunchKernelGGL(k3_block<kFace>, dim3(blocks, 6), dim3(kBlkT), 0, c->stream, k);
+        l += (uint32_t)__builtin_ctz(E) + 1u;
     }
     return hipGetLastError();
 }

@@ -99,6 +99,7 @@ class Context:
         self.specular = specular
         self.aabb_min = tuple(float(x) for x in aabb_min)
         self.extent = float(extent)
+        self.stream = 0          # the HIP stream of set_stream (0: the null stream)
 
     # -- lifetime ---------------------------------------------------------
     def close(self):
@@ -145,6 +146,7 @@ class Context:
 
     def set_stream(self, stream_ptr: int | None):
         self._check(self.lib.vct_set_stream(self.h, C.c_void_p(stream_ptr or 0)), "set_stream")
+        self.stream = stream_ptr or 0
 
     def synchronize(self):
         self._check(self.lib.vct_synchronize(self.h), "synchronize")

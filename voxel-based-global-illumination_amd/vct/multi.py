@@ -110,25 +110,39 @@ class FrameTracer:
     With one rank there is nothing to exchange: the trace writes the frame.
 
     :meth:`frame` is one synchronous frame.  :meth:`step` / :meth:`drain` run
-    frames as a pipeline (RCCL only): the exchange of frame f runs on the
-    process group's stream while frame f+1 is traced, and frame f is
-    un-permuted after that trace was queued.  Two buffer sets alternate; the
-    stream order (trace f+1, wait exchange f, untile f, trace f+2, ...) keeps a
-    buffer from being overwritten before its exchange and untile have read it.
+    frames as a pipeline; a step's outputs are complete (on the caller's
+    current stream) after the next step() or drain().  Two buffer sets
+    alternate.  With `overlap` (default on a GPU; one rank, or several over
+    RCCL) frame f is traced on trace stream f % 2, so the trace of frame f+1
+    starts while the last waves of frame f drain (a K4 launch ends in a tail of
+    few busy CUs; two streams fill it: 1.14x at 1080p on one GPU, 1.37x per
+    rank at 8 ranks, tools/overlap_emul.py) and, over RCCL, the exchange of
+    frame f (issued on the trace stream, so it waits for that trace only) runs
+    beside the trace of frame f+1.  Buffer set b is reused by frame f+2 only
+    after the caller's stream has un-permuted frame f (the trace stream waits
+    for the caller's stream first).  Without overlap the same order runs on
+    one stream: trace f+1, wait exchange f, untile f, trace f+2, ...
     """
 
     def __init__(self, ctx, torch, dist, w: int, h: int, rank: int, world: int, device, mode: str = "present",
-                 root: int = 0):
+                 root: int = 0, overlap=None):
         if mode not in ("present", "allgather"):
             raise ValueError(f"mode {mode!r}: 'present' or 'allgather'")
         self.ctx, self.torch, self.dist = ctx, torch, dist
         self.w, self.h, self.rank, self.world = w, h, rank, world
         self.mode, self.root = mode, root
+        self.device = torch.device(device)
         self.max_tiles = tiles_for_rank(w, h, 0, world)
         self.my_tiles = tiles_for_rank(w, h, rank, world)
         _, _, self.total_tiles = num_tiles(w, h)
+        gpu = self.device.type == "cuda"
+        can = gpu and (world == 1 or self._nccl())
+        if overlap and not can:
+            raise ValueError("overlap: needs a GPU device and one rank or an RCCL group")
+        self.overlap = can if overlap is None else bool(overlap)
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(2)] if self.overlap else None
         f32 = torch.float32
-        nsets = 2 if world > 1 else 1
+        nsets = 2 if (world > 1 or self.overlap) else 1
         tpx = TILE * TILE
         self.comp, self.gath = [], []
         if world > 1 and mode == "allgather":
@@ -144,8 +158,11 @@ class FrameTracer:
                 self.comp = [g[off:off + 2 * self.npx].view(2, self.npx, 4) for g in self.gath]
             else:
                 self.comp = [torch.zeros((2, self.npx, 4), dtype=f32, device=device) for _ in range(nsets)]
-        self.diff = torch.zeros((h, w, 4), dtype=f32, device=device)
-        self.spec = torch.zeros((h, w, 4), dtype=f32, device=device)
+        # one rank: the frames themselves alternate (the trace writes them)
+        self.outs = [(torch.zeros((h, w, 4), dtype=f32, device=device),
+                      torch.zeros((h, w, 4), dtype=f32, device=device)) for _ in range(nsets if world == 1 else 1)]
+        self.diff, self.spec = self.outs[0]
+        self.nsets = nsets
         self.cur = 0
         self.pending = None
 
@@ -156,8 +173,9 @@ class FrameTracer:
 
     def trace_local(self, gb, eye, cone_steps=None, texel_fetches=None, steps_px=None, variant=0, buf=0):
         pos, nrm, alb = gb
-        if self.world == 1:      # the whole frame: straight into the outputs
-            self.ctx.trace_device(pos, nrm, alb, self.w, self.h, eye, self.diff, self.spec,
+        if self.world == 1:      # the whole frame: straight into the outputs of set `buf`
+            d, s = self.outs[buf]
+            self.ctx.trace_device(pos, nrm, alb, self.w, self.h, eye, d, s,
                                   steps_px=steps_px, cone_steps=cone_steps, texel_fetches=texel_fetches,
                                   variant=variant)
             return
@@ -169,10 +187,10 @@ class FrameTracer:
                               tile_rank=self.rank, tile_world=self.world, tile_compact=True, variant=variant)
 
     def _nccl(self):
-        return self.dist.get_backend() == "nccl"
+        return self.world > 1 and self.dist.get_backend() == "nccl"
 
     def _pipelined(self):
-        return self.world > 1 and self._nccl()
+        return self.overlap or self._nccl()
 
     def _exchange(self, buf, async_op):
         """Moves frame `buf`'s tiles; returns the outstanding works (async RCCL) or []."""
@@ -204,7 +222,9 @@ class FrameTracer:
         return works
 
     def _untile(self, buf):
-        if self.mode == "allgather":
+        if self.world == 1:
+            self.diff, self.spec = self.outs[buf]
+        elif self.mode == "allgather":
             self.ctx.untile_planes_device(self.gath[buf], self.w, self.h, self.world, (self.diff, self.spec))
         elif self.rank == self.root:
             self.ctx.untile_planes_device(self.gath[buf], self.w, self.h, self.world, (self.diff, self.spec),
@@ -214,7 +234,7 @@ class FrameTracer:
         """The exchange and the untile of buffer set `buf`, synchronously (also timed alone)."""
         if self.world > 1:
             self._exchange(buf, False)
-            self._untile(buf)
+        self._untile(buf)
 
     def frame(self, gb, eye, variant=0):
         self.drain()
@@ -222,30 +242,61 @@ class FrameTracer:
         self.gather()
         return self.diff, self.spec
 
-    def step(self, gb, eye, variant=0, on_traced=None):
-        """One frame of the pipeline; the frame's outputs are complete after the next step() or drain()."""
+    def step(self, gb, eye, variant=0, events=None):
+        """One frame of the pipeline; the frame's outputs are complete after the next step() or drain().
+        events: (start, end) CUDA events recorded around the frame's trace on the stream it runs on."""
         if not self._pipelined():
+            if events:
+                events[0].record()
             self.trace_local(gb, eye, variant=variant)
-            if on_traced:
-                on_traced()
+            if events:
+                events[1].record()
             self.gather()
             return
         b = self.cur
-        self.cur ^= 1
-        self.trace_local(gb, eye, variant=variant, buf=b)
-        if on_traced:
-            on_traced()
-        works = self._exchange(b, True)
+        self.cur = (b + 1) % self.nsets
+        t = self.torch
+        ts = None
+        if self.overlap:
+            main = t.cuda.current_stream(self.device)
+            saved = self.ctx.stream
+            if saved != main.cuda_stream:
+                raise ValueError("overlap: the context's stream (set_stream) must be the current torch stream")
+            ts = self.streams[b]
+            ts.wait_stream(main)        # the G-buffer, and set b's last untile
+            self.ctx.set_stream(ts.cuda_stream)
+        try:
+            with t.cuda.stream(ts) if ts is not None else _Null():
+                if events:
+                    events[0].record()
+                self.trace_local(gb, eye, variant=variant, buf=b)
+                if events:
+                    events[1].record()
+                works = self._exchange(b, True) if self.world > 1 else []
+        finally:
+            if ts is not None:
+                self.ctx.set_stream(saved)
         self.drain()
-        self.pending = (works, b)
+        self.pending = (works, b, ts)
 
     def drain(self):
+        """Completes the pending frame on the caller's current stream."""
         if self.pending is not None:
-            works, b = self.pending
+            works, b, ts = self.pending
             self.pending = None
             for w in works:
                 w.wait()                                    # current stream waits for the exchange
+            if ts is not None:
+                self.torch.cuda.current_stream(self.device).wait_stream(ts)
             self._untile(b)
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def share_comm_id(dist, rank: int, root: int = 0, get_id=None) -> bytes:
