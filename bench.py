@@ -15,9 +15,9 @@ N > 1, the frame is assembled on the presenting rank 0 (every rank sends
 exactly its own tiles over RCCL; `--exchange allgather` all-gathers to every
 rank instead) and un-permuted there (strong scaling: the frame is fixed, the
 tiles are split).  Frames are pipelined as a renderer's frame loop runs them
-(vct.multi.FrameTracer): frame f is traced on trace stream f % 2, so the next
-frame's trace fills the tail of the previous K4 launch, and the exchange of
-frame f overlaps the trace of frame f+1 (`--no-overlap`: one stream); every
+(vct.multi.FrameTracer): at N > 1 frame f is traced on trace stream f % 2, so
+the next frame's trace fills the tail of the previous K4 launch (`--overlap`),
+and the exchange of frame f overlaps the trace of frame f+1; every
 timed step still traces, exchanges and un-permutes one whole frame, and the
 pipeline is drained inside the timed region.  The roofline's K4 launch
 duration (`k4_kernel_ms_avg`) is timed after the loop with K frames back to
@@ -112,8 +112,8 @@ def parse():
                    help="N = 1: frames of the steady-state hitch loop per G-buffer (0: skip)")
     p.add_argument("--multi-config", default="c4,c5",
                    help="BASELINE configs[3] / [4] measured beside the metric (comma list; empty or 'none': skip)")
-    p.add_argument("--no-overlap", action="store_true",
-                   help="trace every frame on one stream (default: consecutive frames on two streams)")
+    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                   help="consecutive frames on two trace streams (auto: at N > 1 over RCCL)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-json", default=PROFILE)
@@ -419,7 +419,30 @@ def scene_arrays(name):
     return _SCENES[name]
 
 
-def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, counting_only=False):
+def relight_roofline(ctx, n, k2_ms, k3_ms):
+    """HBM fractions of the relight kernels from their algorithmic bytes:
+    K3 reads level 0 once and writes every face of levels 1..L (the block plan builds each
+    subtree in LDS; the subtree tops it reads back are < 0.1 % of that); K2 reads the
+    albedo / normal of every occupied voxel (32 B) and writes its level-0 texel (16 B);
+    its shadow walk reads the 2 MiB occupancy bitmask from L2, not counted."""
+    import numpy as np
+    L = int(math.log2(n))
+    k3_bytes = n ** 3 * 16 + sum(6 * (n >> l) ** 3 * 16 for l in range(1, L + 1))
+    ao, _ = ctx.download_voxels()
+    occ = int(np.count_nonzero(ao[..., 3] > 0))
+    k2_bytes = occ * 48
+    out = {}
+    for name, b, ms, bound in (("k3", k3_bytes, k3_ms, "hbm"), ("k2", k2_bytes, k2_ms, "shadow-walk latency")):
+        gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else None
+        out[f"{name}_roofline"] = {"bound": bound, "bytes": b, "achieved": round(gbs, 1) if gbs else None,
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None}
+    out["k2_roofline"]["occupied_voxels"] = occ
+    return out
+
+
+def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, counting_only=False,
+                  relight_roofs=False):
     """K1-K3 for `scene_name`, the G-buffer, one counting frame, then K timed frames."""
     import numpy as np
     from vct import scenes
@@ -469,6 +492,8 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     ctx.build_mips()
     k3_ms = timed(ctx.build_mips)
     r.update({"k2_inject_ms": round(k2_ms, 3), "k3_mips_ms": round(k3_ms, 3), "grid_bcast_ms": round(bcast_ms, 3)})
+    if relight_roofs:
+        r.update(relight_roofline(ctx, n, k2_ms, k3_ms))
 
     cam = Camera()
     eye = [float(x) for x in cam.position]
@@ -482,7 +507,7 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     torch.cuda.synchronize()
 
     tracer = FrameTracer(ctx, torch, dist, w, h, rank, world, dev, mode=args.exchange,
-                         overlap=False if args.no_overlap else None)
+                         overlap={"auto": None, "on": True, "off": False}[args.overlap])
     # counting pass (same kernel, counters on): frame cone steps and texel fetches
     cnt = torch.zeros(2, dtype=torch.int64, device=dev)
     steps_px = torch.zeros((h, w), dtype=torch.int32, device=dev)
@@ -798,7 +823,7 @@ def run(args, world):
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream.cuda_stream)
 
-    m = measure_scene(args, torch, dist, ctx, args.scene, rank, world, dev, stream)
+    m = measure_scene(args, torch, dist, ctx, args.scene, rank, world, dev, stream, relight_roofs=rank == 0)
     key = profile_key(n, w, h, args.scene, args.gbuffer, args.n_diffuse, spec, args.variant, world)
     rec, reason = load_profile(args.profile_json, key)
     roof = roofline(rec, reason, m["k4_kernel_ms_avg"], m["local_texels"], m["local_valid"], args.profile_json, key)
@@ -835,7 +860,7 @@ def run(args, world):
         result["k4_form"] = form_name(m["k4_form"])
         for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
                    "frame_relight_bcast_ms", "frame_relight_replicated_ms", "replicated_k2_equals_bcast",
-                   "trace_ms_max_rank", "gather_ms", "allgather_ms"):
+                   "trace_ms_max_rank", "gather_ms", "allgather_ms", "k2_roofline", "k3_roofline"):
             if k_ in m:
                 result[k_] = m[k_]
         result["roofline"] = roof

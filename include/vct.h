@@ -19,7 +19,13 @@
  *    single-threaded: engine.h:7, assets.h:13).  A ctx owns every device buffer.
  *  - Host-pointer entry points are synchronous on return.  *_device entry
  *    points take device pointers and are asynchronous on the ctx stream
- *    (vct_set_stream); vct_synchronize() waits for them.
+ *    (vct_set_stream); vct_synchronize() waits for them.  A host may switch
+ *    the ctx stream between vct_trace_device calls so that consecutive frames
+ *    run concurrently on different streams (vct.multi.FrameTracer does, for
+ *    1.14x at 1080p): the trace's scratch belongs to the stream (4 streams;
+ *    a fifth one frees every set after a device synchronize).  Grid
+ *    updates (voxelize / inject / build_mips / uploads) must be ordered
+ *    against traces on other streams by the host (events).
  *  - Data layouts: grids cross the ABI linear-Z RGBA32F, index x + n*(y + n*z)
  *    (the device copy is bricked, see vct_level0_device); the G-buffer and
  *    outputs are [h][w][4] float, row 0 = top of the image.
@@ -202,9 +208,12 @@ vct_status vct_trace_device(vct_ctx* ctx, const vct_trace_args* args);
  * choice per workload (frame size, tiling, cone set, grid size; up to four workloads,
  * least recently used replaced): a new workload's first counter-free launches time the
  * candidates (while timing, each launch waits for the previous timed one), then the
- * fastest is kept.  Afterwards launches never block: every 16th is timed with events
- * that are only polled, and the workload is timed again only when its time drifts above
- * 1.35x the settled time three samples in a row (the scene or the G-buffer changed).
+ * fastest is kept.  Afterwards launches never block: every 2nd is timed with events
+ * that are only polled, and the workload is timed again when its time drifts above
+ * 1.35x the settled time three samples in a row (the G-buffer changed), or after a new
+ * voxelization once the choice has served 16 launches (doubling, up to 4096, each time
+ * the new scene keeps the winner).  Launches on two streams (overlapped frames) are not
+ * watched, and a timing launch then also waits for the previous launch of any stream.
  * Returns the kept candidate of the last traced workload -- bit 0 the form (0 union,
  * 1 occupancy), bit 1 ray reordering; a forced candidate when the variant fixes both --
  * or -1 while it is still being timed. */

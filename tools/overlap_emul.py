@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--scene", default="atrium")
+    ap.add_argument("--variant", type=lambda v: int(v, 0), default=0,
+                    help="trace variant (0x1000000 union form, 0x2000000 occupancy form)")
     a = ap.parse_args()
     import torch
     from vct import Context, scenes
@@ -44,7 +46,7 @@ def main():
     for W in [int(x) for x in a.worlds.split(",")]:
         npx = tiles_for_rank(a.w, a.h, 0, W) * TILE * TILE if W > 1 else a.w * a.h
         bufs = [(torch.empty((npx, 4), device=dev), torch.empty((npx, 4), device=dev)) for _ in range(2)]
-        kw = dict(tile_rank=0, tile_world=W, tile_compact=W > 1)
+        kw = dict(tile_rank=0, tile_world=W, tile_compact=W > 1, variant=a.variant)
 
         def launch(b, stream):
             ctx.set_stream(stream.cuda_stream)

@@ -282,6 +282,7 @@ void vct_destroy(vct_ctx* c) {
             for (auto& sl : f)
                 for (hipEvent_t e : sl)
                     if (e) (void)hipEventDestroy(e);
+    if (c->k4tune.prev_end) (void)hipEventDestroy(c->k4tune.prev_end);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -1425,9 +1425,19 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
         t.chosen = cands_in[0];
         return cands_in[0];
     }
+    bool overlapped = false;                     // the previous launch (another stream) still runs
+    if (timed) {
+        if (T.prev_stream && T.prev_stream != c->stream) T.multi = true;
+        T.prev_stream = c->stream;
+        if (T.multi && T.prev_end) overlapped = hipEventQuery(T.prev_end) == hipErrorNotReady;
+    }
     if (t.chosen < 0 && timed && t.last) {       // while timing: this entry's previous timed launch first
         (void)hipEventSynchronize(t.last);
         t.last = nullptr;
+    }
+    if (t.chosen < 0 && timed && overlapped) {   // ... and the previous launch of any stream
+        (void)hipEventSynchronize(T.prev_end);
+        overlapped = false;
     }
     for (int f = 0; f < 4; ++f)                  // harvest completed samples (non-blocking)
         for (int sl = 0; sl < K4Tuner::kSlots; ++sl) {
@@ -1469,7 +1479,9 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
     const int* cands = cands_in;
     const int n = n_in;
     if (t.chosen >= 0) {
-        if (!timed || ++t.since % K4Tuner::kWatchEvery != 0) return t.chosen;
+        // a host overlapping frames on two streams gets no watch: a launch's event time then
+        // depends on how much of it the neighbouring frames shared (measured: false drifts)
+        if (!timed || ++t.since % K4Tuner::kWatchEvery != 0 || T.multi) return t.chosen;
         const int f = t.chosen, sl = t.head[f];
         if (t.busy[f][sl]) return f;
         for (hipEvent_t& ev : t.ev[f][sl])
@@ -1675,6 +1687,10 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
                 else VCT_K4_WG(true, VCT_K4_MIN_WAVES, true, true, false);
             }
             if (ev) (void)hipEventRecord(ev[1], c->stream);
+            K4Tuner& T = c->k4tune;
+            if (deflt && !cnt_form && T.multi && (T.prev_end || hipEventCreateWithFlags(&T.prev_end,
+                                                                          hipEventDisableTiming) == hipSuccess))
+                (void)hipEventRecord(T.prev_end, c->stream);
         }
     }
 #undef VCT_K4

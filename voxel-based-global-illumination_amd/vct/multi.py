@@ -112,11 +112,11 @@ class FrameTracer:
     :meth:`frame` is one synchronous frame.  :meth:`step` / :meth:`drain` run
     frames as a pipeline; a step's outputs are complete (on the caller's
     current stream) after the next step() or drain().  Two buffer sets
-    alternate.  With `overlap` (default on a GPU; one rank, or several over
-    RCCL) frame f is traced on trace stream f % 2, so the trace of frame f+1
-    starts while the last waves of frame f drain (a K4 launch ends in a tail of
-    few busy CUs; two streams fill it: 1.14x at 1080p on one GPU, 1.37x per
-    rank at 8 ranks, tools/overlap_emul.py) and, over RCCL, the exchange of
+    alternate.  With `overlap` (default for several ranks over RCCL; possible
+    for one rank) frame f is traced on trace stream f % 2, so the trace of frame
+    f+1 starts while the last waves of frame f drain (a K4 launch ends in a tail
+    of few busy CUs; two streams fill it: 1.37x per rank of 8 on one GPU,
+    tools/overlap_tracer.py --world 8) and, over RCCL, the exchange of
     frame f (issued on the trace stream, so it waits for that trace only) runs
     beside the trace of frame f+1.  Buffer set b is reused by frame f+2 only
     after the caller's stream has un-permuted frame f (the trace stream waits
@@ -139,7 +139,11 @@ class FrameTracer:
         can = gpu and (world == 1 or self._nccl())
         if overlap and not can:
             raise ValueError("overlap: needs a GPU device and one rank or an RCCL group")
-        self.overlap = can if overlap is None else bool(overlap)
+        # default: overlap the ranks of an RCCL group (a rank's launch is short, its tail long:
+        # 1.37x per rank of 8, tools/overlap_tracer.py --world 8); one rank traces on one
+        # stream (a full 1080p frame gains 0-6 % by hand and loses up to 8 % through this
+        # driver, depending on which hardware queues the streams land on)
+        self.overlap = (can and world > 1) if overlap is None else bool(overlap)
         self.streams = [torch.cuda.Stream(self.device) for _ in range(2)] if self.overlap else None
         f32 = torch.float32
         nsets = 2 if (world > 1 or self.overlap) else 1
