@@ -15,9 +15,11 @@ N > 1, the frame is assembled on the presenting rank 0 (every rank sends
 exactly its own tiles over RCCL; `--exchange allgather` all-gathers to every
 rank instead) and un-permuted there (strong scaling: the frame is fixed, the
 tiles are split).  Frames are pipelined as a renderer's frame loop runs them
-(vct.multi.FrameTracer): at N > 1 frame f is traced on trace stream f % 2, so
-the next frame's trace fills the tail of the previous K4 launch (`--overlap`),
-and the exchange of frame f overlaps the trace of frame f+1; every
+(vct.multi.FrameTracer): the exchange of frame f overlaps the trace of frame
+f+1, and frame f may be traced on trace stream f % 2, so that the next frame's
+trace fills the tail of the previous K4 launch -- FrameTracer.tune times both
+before the warmup and keeps the faster (`overlap_tune`; `--overlap on|off`
+forces it); every
 timed step still traces, exchanges and un-permutes one whole frame, and the
 pipeline is drained inside the timed region.  The roofline's K4 launch
 duration (`k4_kernel_ms_avg`) is timed after the loop with K frames back to
@@ -113,7 +115,7 @@ def parse():
     p.add_argument("--multi-config", default="c4,c5",
                    help="BASELINE configs[3] / [4] measured beside the metric (comma list; empty or 'none': skip)")
     p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
-                   help="consecutive frames on two trace streams (auto: at N > 1 over RCCL)")
+                   help="consecutive frames on two trace streams (auto: FrameTracer.tune decides)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-json", default=PROFILE)
@@ -352,6 +354,15 @@ def max_over_ranks(torch, dist, dev, vals, world):
     return [float(x) for x in t.tolist()]
 
 
+_T0 = time.perf_counter()
+
+
+def progress(rank, what):
+    """one line per phase on stderr (rank 0): a long run keeps writing while it works"""
+    if rank == 0:
+        print(f"[bench {time.perf_counter() - _T0:7.1f} s] {what}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "0") or 0)
@@ -526,6 +537,8 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     # the context times the two compiled forms of K4 on its first counter-free launches of a
     # workload and keeps the faster (vct_trace_form); let that settle before the warmup
     r["k4_form"] = settle_form(ctx, torch, lambda: tracer.trace_local(gb, eye, variant=args.variant))
+    # one stream or two (FrameTracer.tune: 16 + 16 timed frames, before the warmup)
+    r["overlap_tune"] = tracer.tune(gb, eye, variant=args.variant) if tracer.auto else None
     for _ in range(args.warmup):
         tracer.frame(gb, eye, variant=args.variant)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -672,7 +685,7 @@ def measure_config(args, torch, dist, rank, world, dev, stream, cfg):
                        f"{a.width}x{a.height}, {a.n_diffuse}+{0 if args.no_spec else 1} cones",
            "value": round(m["value"], 2), "unit": "Mcone-steps/s", "ms_per_step": round(m["ms_per_step"], 4),
            "frame_cone_steps": m["frame_cone_steps"], "k4_kernel_ms_avg_rank0": round(m["k4_kernel_ms_avg"], 4),
-           "k4_form_rank0": form_name(m["k4_form"])}
+           "k4_form_rank0": form_name(m["k4_form"]), "overlap_tune_rank0": m["overlap_tune"]}
     for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
                "replicated_k2_equals_bcast", "trace_ms_max_rank", "gather_ms", "allgather_ms"):
         if k_ in m:
@@ -823,7 +836,9 @@ def run(args, world):
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream.cuda_stream)
 
+    progress(rank, f"metric workload: {args.scene} {n}^3 {w}x{h}, {world} rank(s)")
     m = measure_scene(args, torch, dist, ctx, args.scene, rank, world, dev, stream, relight_roofs=rank == 0)
+    progress(rank, f"metric done: {m['value']:.0f} Mcone-steps/s")
     key = profile_key(n, w, h, args.scene, args.gbuffer, args.n_diffuse, spec, args.variant, world)
     rec, reason = load_profile(args.profile_json, key)
     roof = roofline(rec, reason, m["k4_kernel_ms_avg"], m["local_texels"], m["local_valid"], args.profile_json, key)
@@ -857,6 +872,7 @@ def run(args, world):
         result["k4_kernel_ms_median"] = round(m["k4_kernel_ms_median"], 4)
         result["k4_kernel_ms_avg_overlapped"] = round(m["k4_kernel_ms_avg_overlapped"], 4)
         result["frame_overlap"] = "two trace streams" if m["overlap"] else "one stream"
+        result["overlap_tune"] = m["overlap_tune"]
         result["k4_form"] = form_name(m["k4_form"])
         for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
                    "frame_relight_bcast_ms", "frame_relight_replicated_ms", "replicated_k2_equals_bcast",
@@ -873,6 +889,7 @@ def run(args, world):
     if world == 1 and args.frame_loop:
         loop_scene = frame_loop(torch, ctx, m["_gb"], w, h, m["_eye"], stream, args.frame_loop, variant=args.variant)
         result["frame_loop"] = {f"G_{args.gbuffer}": loop_scene}
+        progress(rank, "frame loop done")
     capi = None
     if world > 1:
         if os.environ.get("VCT_DIST_BACKEND", "nccl") == "nccl":
@@ -887,6 +904,7 @@ def run(args, world):
     torch.cuda.empty_cache()
     st = (args.stress or "").strip()
     if st == "rand" and world == 1 and args.gbuffer == "scene":
+        progress(rank, "stress (G_rand)")
         result["stress"] = stress_rand(args, torch, ctx, dev, stream)
         loop = result["stress"].pop("_loop")
         if loop is not None:
@@ -895,6 +913,7 @@ def run(args, world):
     sec = (args.secondary or "").strip()
     if sec and sec != "none" and sec != args.scene:
         # the same size on a non-flat scene (varied normals: fewer combined-face bricks)
+        progress(rank, f"secondary: {sec}")
         s2 = measure_scene(args, torch, dist, ctx, sec, rank, world, dev, stream)
         if rank == 0:
             result["secondary"] = {
@@ -915,6 +934,7 @@ def run(args, world):
             cfg = MULTI_CONFIGS[name]
             if cfg["ranks"] is not None and world not in cfg["ranks"]:
                 continue
+            progress(rank, f"multi_config {name}")
             out[name] = measure_config(args, torch, dist, rank, world, dev, stream, cfg)
         if rank == 0:
             result["multi_config"] = out

@@ -212,8 +212,9 @@ vct_status vct_trace_device(vct_ctx* ctx, const vct_trace_args* args);
  * that are only polled, and the workload is timed again when its time drifts above
  * 1.35x the settled time three samples in a row (the G-buffer changed), or after a new
  * voxelization once the choice has served 16 launches (doubling, up to 4096, each time
- * the new scene keeps the winner).  Launches on two streams (overlapped frames) are not
- * watched, and a timing launch then also waits for the previous launch of any stream.
+ * the new scene keeps the winner).  While launches alternate streams (overlapped frames;
+ * until 64 launches after the last switch) they are not watched, and a timing launch
+ * then also waits for the previous launch of any stream.
  * Returns the kept candidate of the last traced workload -- bit 0 the form (0 union,
  * 1 occupancy), bit 1 ray reordering; a forced candidate when the variant fixes both --
  * or -1 while it is still being timed. */

@@ -449,6 +449,38 @@ def test_frame_pipeline_equals_full_frames(gpu_ready, world, mode, overlap):
     ctx.close()
 
 
+def test_frame_tracer_tune(gpu_ready):
+    """FrameTracer's default (overlap=None) times one stream against two on its first step
+    and keeps the faster; either way the frames stay bit-identical to single traces."""
+    import torch
+    from vct import scenes
+    from vct.camera import Camera
+    from vct.multi import FrameTracer
+    ctx, s, arrs, (g0, E) = gpu_pipeline(32, "atrium")
+    w, h = 200, 130
+    cam = Camera()
+    dev = torch.device("cuda")
+    gb = tuple(torch.empty((h, w, 4), device=dev) for _ in range(3))
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.gbuffer_raycast_device(cam, w, h, scenes.ROUGHNESS, *gb)
+    eyes = [[float(cam.position[0]) + 0.05 * f, float(cam.position[1]), float(cam.position[2])] for f in range(3)]
+    refs = []
+    for e in eyes:
+        d, sp = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+        ctx.trace_device(*gb, w, h, e, d, sp)
+        refs.append((d, sp))
+    tr = FrameTracer(ctx, torch, None, w, h, 0, 1, dev)
+    assert tr.auto and tr.tuned is None
+    for f, e in enumerate(eyes):
+        tr.step(gb, e)
+        if f == 0:
+            assert not tr.auto and set(tr.tuned) == {"one_stream_ms", "two_streams_ms", "overlap"}
+    tr.drain()
+    torch.cuda.synchronize()
+    assert torch.equal(tr.diff, refs[-1][0]) and torch.equal(tr.spec, refs[-1][1])
+    ctx.close()
+
+
 def test_raycast_matches_numpy(gpu_ready):
     import torch
     from vct import scenes

@@ -6,7 +6,10 @@
 For each world size N and each rank r < N, times exactly the launch rank r
 makes in the N-GPU bench (its interleaved 64x64 tiles, rank-compact output) and
 reports the slowest rank: the K4 part of the N-GPU step (the all-gather and
-the untile come on top; the gather overlaps the next frame's trace).
+the untile come on top; the gather overlaps the next frame's trace).  For N > 1 it
+also reports each rank's K4 time per frame when, as in vct.multi.FrameTracer at
+N > 1, consecutive frames run on two streams (`k4_ms_per_frame_overlapped_*`: the
+next frame's waves fill the launch's tail).
 
     python tools/rank_emul.py --pmc-world N [--pmc-rank 0] [--pmc-launches 20]
 
@@ -54,7 +57,15 @@ def main():
 
     def timed(fn):
         ts = []
-        fn()
+        last, run = None, 0
+        for _ in range(256):                  # let the context's choice for this launch settle
+            fn()
+            torch.cuda.synchronize()
+            f = ctx.trace_form
+            run = run + 1 if (f >= 0 and f == last) else 0
+            last = f
+            if run >= 8:
+                break
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -88,11 +99,33 @@ def main():
         for r in range(W):
             per.append(timed(lambda: ctx.trace_device(*gb, a.w, a.h, cam.position, buf[0], buf[1], tile_rank=r,
                                                       tile_world=W, tile_compact=W > 1, variant=a.variant)))
+        ov = []
+        if W > 1:
+            bufs = [torch.empty((2, maxt * TILE * TILE, 4), device=dev) for _ in range(2)]
+            streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+            frames = 40
+            for r in range(W):
+                def loop():
+                    for f in range(frames):
+                        st = streams[f % 2]
+                        st.wait_stream(stream)
+                        ctx.set_stream(st.cuda_stream)
+                        b = bufs[f % 2]
+                        ctx.trace_device(*gb, a.w, a.h, cam.position, b[0], b[1], tile_rank=r, tile_world=W,
+                                         tile_compact=True, variant=a.variant)
+                        ctx.set_stream(stream.cuda_stream)
+                        stream.wait_stream(streams[(f + 1) % 2])
+                    stream.wait_stream(streams[0])
+                    stream.wait_stream(streams[1])
+                ov.append(timed(loop) / frames)
         gath = torch.empty((W, 2, maxt * TILE * TILE, 4), device=dev)
         fr = (torch.empty((a.h, a.w, 4), device=dev), torch.empty((a.h, a.w, 4), device=dev))
         unt = timed(lambda: ctx.untile_planes_device(gath, a.w, a.h, W, fr)) if W > 1 else 0.0
         out[W] = {"k4_ms_max_rank": round(max(per), 4), "k4_ms_min_rank": round(min(per), 4),
                   "tiles_per_rank": maxt, "untile_ms": round(unt, 4)}
+        if ov:
+            out[W].update({"k4_ms_per_frame_overlapped_max_rank": round(max(ov), 4),
+                           "k4_ms_per_frame_overlapped_min_rank": round(min(ov), 4)})
     base = out.get(1, {}).get("k4_ms_max_rank")
     if base:
         for W, d in out.items():

@@ -91,10 +91,11 @@ constexpr int kStreamSets = 4;
 // of each candidate (its code is loaded already) and drops a candidate after one sample
 // that is kCompetitive times slower than the best so far: a much slower candidate
 // (screen order on an incoherent G-buffer: 6x) costs one frame per re-timing.
-// Once timed launches come on two streams (a host overlapping frames, vct.h conventions)
-// the entry is not watched (a launch's event time then includes whatever share of the chip
-// the neighbouring frames took: measured false drifts), and a timing launch first waits
-// for the previous launch of any stream.  VCT_TUNE_LOG=1 prints every decision to stderr.
+// While timed launches alternate streams (a host overlapping frames, vct.h conventions;
+// until 64 launches after the last switch) the entries are not watched (a launch's event
+// time then includes whatever share of the chip the neighbouring frames took: measured
+// false drifts), and a timing launch first waits for the previous launch of any stream.
+// VCT_TUNE_LOG=1 prints every decision to stderr.
 struct K4Tuner {
     static constexpr int kSlots = 4;          // event pairs in flight per candidate
     static constexpr int kSamples = 2;        // timed samples per candidate after the first (cold) one
@@ -129,9 +130,11 @@ struct K4Tuner {
     uint64_t clock = 0;
     // concurrent frames: once timed launches have come on two streams, each one records
     // `prev_end`, and a timing launch first waits for it (samples stay isolated)
+    static constexpr uint64_t kMultiLaunches = 64;   // a stream switch counts for this many launches
     hipStream_t prev_stream = nullptr;
     hipEvent_t prev_end = nullptr;
-    bool multi = false;
+    uint64_t multi_until = 0;                 // clock value up to which launches count as overlapped
+    bool multi = false;                       // clock < multi_until at the last launch
 };
 
 }  // namespace vct

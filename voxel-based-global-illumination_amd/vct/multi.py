@@ -112,16 +112,22 @@ class FrameTracer:
     :meth:`frame` is one synchronous frame.  :meth:`step` / :meth:`drain` run
     frames as a pipeline; a step's outputs are complete (on the caller's
     current stream) after the next step() or drain().  Two buffer sets
-    alternate.  With `overlap` (default for several ranks over RCCL; possible
-    for one rank) frame f is traced on trace stream f % 2, so the trace of frame
-    f+1 starts while the last waves of frame f drain (a K4 launch ends in a tail
-    of few busy CUs; two streams fill it: 1.37x per rank of 8 on one GPU,
-    tools/overlap_tracer.py --world 8) and, over RCCL, the exchange of
-    frame f (issued on the trace stream, so it waits for that trace only) runs
-    beside the trace of frame f+1.  Buffer set b is reused by frame f+2 only
-    after the caller's stream has un-permuted frame f (the trace stream waits
-    for the caller's stream first).  Without overlap the same order runs on
-    one stream: trace f+1, wait exchange f, untile f, trace f+2, ...
+    alternate.  With `overlap` frame f is traced on trace stream f % 2, so the
+    trace of frame f+1 starts while the last waves of frame f drain (a K4 launch
+    ends in a tail of few busy CUs) and, over RCCL, the exchange of frame f
+    (issued on the trace stream, so it waits for that trace only) runs beside
+    the trace of frame f+1.  Buffer set b is reused by frame f+2 only after the
+    caller's stream has un-permuted frame f (the trace stream waits for the
+    caller's stream first).  Without overlap the same order runs on one stream:
+    trace f+1, wait exchange f, untile f, trace f+2, ...
+
+    Whether overlap pays depends on the launch: measured on one MI355X
+    (tools/rank_emul.py, tools/overlap_tracer.py) a rank's 1080p launch of an
+    8-rank split gains 1.42x and one of 2 ranks 1.11x, one of 4 ranks loses 4 %,
+    a full 1080p frame loses up to 8 % and a 4K frame gains ~5 %.  So
+    `overlap=None` (default, one rank or an RCCL group on a GPU) decides by
+    timing: :meth:`tune` runs 16 pipelined frames each way and keeps overlap if
+    it is 3 % faster; an untuned tracer tunes on its first step().
     """
 
     def __init__(self, ctx, torch, dist, w: int, h: int, rank: int, world: int, device, mode: str = "present",
@@ -139,14 +145,13 @@ class FrameTracer:
         can = gpu and (world == 1 or self._nccl())
         if overlap and not can:
             raise ValueError("overlap: needs a GPU device and one rank or an RCCL group")
-        # default: overlap the ranks of an RCCL group (a rank's launch is short, its tail long:
-        # 1.37x per rank of 8, tools/overlap_tracer.py --world 8); one rank traces on one
-        # stream (a full 1080p frame gains 0-6 % by hand and loses up to 8 % through this
-        # driver, depending on which hardware queues the streams land on)
-        self.overlap = (can and world > 1) if overlap is None else bool(overlap)
-        self.streams = [torch.cuda.Stream(self.device) for _ in range(2)] if self.overlap else None
+        self.auto = overlap is None and can          # decided by tune()
+        self.tuned = None
+        self.overlap = bool(overlap)
+        two = can and overlap is not False
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(2)] if two else None
         f32 = torch.float32
-        nsets = 2 if (world > 1 or self.overlap) else 1
+        nsets = 2 if (world > 1 or two) else 1
         tpx = TILE * TILE
         self.comp, self.gath = [], []
         if world > 1 and mode == "allgather":
@@ -246,9 +251,39 @@ class FrameTracer:
         self.gather()
         return self.diff, self.spec
 
+    def tune(self, gb, eye, variant=0, frames=16, gain=1.03):
+        """Times `frames` pipelined frames on one stream and as many overlapped (after one
+        untimed frame each), keeps overlap if it is `gain` times faster; returns the two
+        ms / frame.  Every rank of a group must call it (the frames exchange)."""
+        t = self.torch
+        if self.streams is None:
+            return None
+        self.auto = False                             # step() below runs the chosen mode
+        main = t.cuda.current_stream(self.device)
+        ms = {}
+        for ov in (False, True):
+            self.drain()
+            self.overlap = ov
+            self.step(gb, eye, variant=variant)
+            self.drain()
+            e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+            e0.record(main)
+            for _ in range(frames):
+                self.step(gb, eye, variant=variant)
+            self.drain()
+            e1.record(main)
+            e1.synchronize()
+            ms[ov] = e0.elapsed_time(e1) / frames
+        self.overlap = ms[True] * gain < ms[False]
+        self.tuned = {"one_stream_ms": round(ms[False], 4), "two_streams_ms": round(ms[True], 4),
+                      "overlap": self.overlap}
+        return self.tuned
+
     def step(self, gb, eye, variant=0, events=None):
         """One frame of the pipeline; the frame's outputs are complete after the next step() or drain().
         events: (start, end) CUDA events recorded around the frame's trace on the stream it runs on."""
+        if self.auto:
+            self.tune(gb, eye, variant=variant)
         if not self._pipelined():
             if events:
                 events[0].record()
