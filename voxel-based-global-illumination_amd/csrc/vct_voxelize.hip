@@ -508,6 +508,7 @@ __global__ void __launch_bounds__(256) k2_coarse(const unsigned long long* __res
 
 // A.3 shadow walk with the coarse bits (LDS) in front of the fine word: the
 // dda_visibility() sequence, cell for cell
+template <int kB>
 __device__ __forceinline__ float dda_coarse(const unsigned long long* __restrict__ bits, const uint32_t* __restrict__ cb,
                                             int N, int cs, int cn, float qx, float qy, float qz, float lx, float ly,
                                             float lz) {
@@ -528,7 +529,6 @@ __device__ __forceinline__ float dda_coarse(const unsigned long long* __restrict
     // branch-free (selects, no exec-mask branches), then looked up together.
     // A cell counts only while the walk is inside the grid; any occupied counted
     // cell blocks the light (the walk stops at the first one either way).
-    constexpr int kB = 8;
     for (;;) {
         uint32_t cv[kB], cc[kB];
         bool in[kB];
@@ -569,8 +569,10 @@ __device__ __forceinline__ float dda_coarse(const unsigned long long* __restrict
 
 constexpr int kCoarseWords = 64 * 64 * 64 / 32;   // 32 KiB of LDS
 
-// one lane per lit voxel; 1024-thread blocks share one LDS copy of the coarse bits
-__global__ void __launch_bounds__(1024) k2_walk(const uint32_t* __restrict__ lit, const uint32_t* __restrict__ n_lit,
+// one lane per lit voxel; BS-thread blocks share one LDS copy of the coarse bits; KB cells
+// per lookup batch
+template <int KB, int BS>
+__global__ void __launch_bounds__(BS) k2_walk(const uint32_t* __restrict__ lit, const uint32_t* __restrict__ n_lit,
                                                 const uint32_t* __restrict__ coarse, int cs,
                                                 const float4* __restrict__ albedo_occ,
                                                 const float4* __restrict__ normal,
@@ -580,17 +582,17 @@ __global__ void __launch_bounds__(1024) k2_walk(const uint32_t* __restrict__ lit
     __shared__ uint32_t cbits[kCoarseWords];
     const int cn = n >> cs;
     const uint32_t ncw = ((uint32_t)cn * cn * cn + 31) / 32;
-    for (uint32_t i = threadIdx.x; i < ncw; i += 1024) cbits[i] = coarse[i];
+    for (uint32_t i = threadIdx.x; i < ncw; i += BS) cbits[i] = coarse[i];
     __syncthreads();
     const uint32_t cnt = *n_lit;
-    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < cnt; i += gridDim.x * 1024) {
+    for (uint32_t i = blockIdx.x * BS + threadIdx.x; i < cnt; i += gridDim.x * BS) {
         const uint32_t v = lit[i];
         const float4 ao = albedo_occ[v];
         const float4 nm = normal[v];
         const float ndl = dot3(nm.x, nm.y, nm.z, lx, ly, lz);
         const int x = (int)(v % (uint32_t)n), y = (int)((v / (uint32_t)n) % (uint32_t)n),
                   z = (int)(v / ((uint32_t)n * (uint32_t)n));
-        const float vis = dda_coarse(bits, cbits, n, cs, cn, ((float)x + 0.5f) + nm.x, ((float)y + 0.5f) + nm.y,
+        const float vis = dda_coarse<KB>(bits, cbits, n, cs, cn, ((float)x + 0.5f) + nm.x, ((float)y + 0.5f) + nm.y,
                                      ((float)z + 0.5f) + nm.z, lx, ly, lz);
         r0[l0_texel(v, (uint32_t)n)] =
             make_float4(((ao.x * cr) * ndl) * vis, ((ao.y * cg) * ndl) * vis, ((ao.z * cb) * ndl) * vis, 1.0f);
@@ -730,8 +732,32 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
     const uint32_t blocks = (uint32_t)std::min<size_t>((nv / 64 + 255) / 256 + 1, 4096);
     hipLaunchKernelGGL(k2_shade, dim3(blocks), dim3(256), 0, s, g.occ_list, g.occ_count, g.normal, lx, ly, lz, lit,
                        counts, g.pyr, g.n);
-    hipLaunchKernelGGL(k2_walk, dim3(512), dim3(1024), 0, s, lit, counts, coarse, cs,
-                       g.albedo_occ, g.normal, g.occ_bits, (int)g.n, lx, ly, lz, cr, cg, cb, g.pyr);
+    // A/B (VCT_K2_WALK = batch cells * 10000 + block threads, VCT_K2_GRID = blocks): default
+    // 16 cells per lookup batch, 256-thread blocks, 2048 of them.  Measured (tools/k2_bench.py,
+    // 256^3): atrium 0.186 -> 0.143 ms, courtyard 0.195 -> 0.181 ms against 8 cells x 1024
+    // threads: smaller blocks finish their slowest wave sooner and free the CU for the next
+    static const int walk = [] {
+        const char* v = getenv("VCT_K2_WALK");
+        return v ? atoi(v) : 160256;
+    }();
+    static const uint32_t wgrid = [] {
+        const char* v = getenv("VCT_K2_GRID");
+        return v ? (uint32_t)atoi(v) : 0u;
+    }();
+#define VCT_K2_WALK_LAUNCH(KB, BS)                                                                               \
+    hipLaunchKernelGGL((k2_walk<KB, BS>), dim3(wgrid ? wgrid : 512u * 1024u / BS), dim3(BS), 0, s, lit, counts,   \
+                       coarse, cs, g.albedo_occ, g.normal, g.occ_bits, (int)g.n, lx, ly, lz, cr, cg, cb, g.pyr)
+    switch (walk) {
+        case 160128: VCT_K2_WALK_LAUNCH(16, 128); break;
+        case 160512: VCT_K2_WALK_LAUNCH(16, 512); break;
+        case 161024: VCT_K2_WALK_LAUNCH(16, 1024); break;
+        case 80256: VCT_K2_WALK_LAUNCH(8, 256); break;
+        case 40256: VCT_K2_WALK_LAUNCH(4, 256); break;
+        case 41024: VCT_K2_WALK_LAUNCH(4, 1024); break;
+        case 81024: VCT_K2_WALK_LAUNCH(8, 1024); break;
+        default: VCT_K2_WALK_LAUNCH(16, 256); break;
+    }
+#undef VCT_K2_WALK_LAUNCH
     return hipGetLastError();
 }
 
