@@ -121,13 +121,13 @@ class FrameTracer:
     caller's stream first).  Without overlap the same order runs on one stream:
     trace f+1, wait exchange f, untile f, trace f+2, ...
 
-    Whether overlap pays depends on the launch: measured on one MI355X
-    (tools/rank_emul.py, tools/overlap_tracer.py) a rank's 1080p launch of an
-    8-rank split gains 1.42x and one of 2 ranks 1.11x, one of 4 ranks loses 4 %,
-    a full 1080p frame loses up to 8 % and a 4K frame gains ~5 %.  So
-    `overlap=None` (default, one rank or an RCCL group on a GPU) decides by
-    timing: :meth:`tune` runs 16 pipelined frames each way and keeps overlap if
-    it is 3 % faster; an untuned tracer tunes on its first step().
+    Whether overlap pays depends on the launch and on the hardware queues the
+    two streams land on, so `overlap=None` (default, one rank or an RCCL group
+    on a GPU) decides by timing: :meth:`tune` runs 16 pipelined frames on one
+    stream and on two stream pairs (normal and high priority) and keeps the
+    fastest overlap if it is 1.5 % faster; an untuned tracer tunes on its first
+    step().  Measured on one MI355X: 1080p full frame 1.170 -> 1.127 ms, a
+    rank's launch of an 8-rank split 0.243 -> 0.172 ms, 4K 4.97 -> 4.82 ms.
     """
 
     def __init__(self, ctx, torch, dist, w: int, h: int, rank: int, world: int, device, mode: str = "present",
@@ -251,20 +251,30 @@ class FrameTracer:
         self.gather()
         return self.diff, self.spec
 
-    def tune(self, gb, eye, variant=0, frames=16, gain=1.03):
-        """Times `frames` pipelined frames on one stream and as many overlapped (after one
-        untimed frame each), keeps overlap if it is `gain` times faster; returns the two
-        ms / frame.  Every rank of a group must call it (the frames exchange)."""
+    def tune(self, gb, eye, variant=0, frames=16, gain=1.015, warm=8):
+        """Times `frames` pipelined frames on one stream and as many overlapped on each of two
+        stream pairs (normal and high priority; after `warm` untimed frames each: the first
+        launches on a fresh stream pay a one-time cost), keeps the
+        fastest overlap if it is `gain` times faster than one stream; returns the ms / frame.
+        Which hardware queues a pair lands on matters (measured on one MI355X, 1080p: one
+        normal pair 1.21 ms, another 1.11, a high-priority pair 1.12, one stream 1.17), hence
+        the timing; without the warm frames the first launches on the fresh streams made
+        overlap look 25 % slower.  Every rank of a group must call it (the frames exchange)."""
         t = self.torch
         if self.streams is None:
             return None
         self.auto = False                             # step() below runs the chosen mode
         main = t.cuda.current_stream(self.device)
+        pairs = {"one stream": None, "two streams": self.streams,
+                 "two high-priority streams": [t.cuda.Stream(self.device, priority=-1) for _ in range(2)]}
         ms = {}
-        for ov in (False, True):
+        for name, pair in pairs.items():
             self.drain()
-            self.overlap = ov
-            self.step(gb, eye, variant=variant)
+            self.overlap = pair is not None
+            if pair is not None:
+                self.streams = pair
+            for _ in range(warm):
+                self.step(gb, eye, variant=variant)
             self.drain()
             e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
             e0.record(main)
@@ -273,10 +283,13 @@ class FrameTracer:
             self.drain()
             e1.record(main)
             e1.synchronize()
-            ms[ov] = e0.elapsed_time(e1) / frames
-        self.overlap = ms[True] * gain < ms[False]
-        self.tuned = {"one_stream_ms": round(ms[False], 4), "two_streams_ms": round(ms[True], 4),
-                      "overlap": self.overlap}
+            ms[name] = e0.elapsed_time(e1) / frames
+        best = min(("two streams", "two high-priority streams"), key=lambda k: ms[k])
+        self.overlap = ms[best] * gain < ms["one stream"]
+        self.streams = pairs[best]
+        self.tuned = {k.replace(" ", "_").replace("-", "_") + "_ms": round(v, 4) for k, v in ms.items()}
+        self.tuned["chosen"] = best if self.overlap else "one stream"
+        self.tuned["overlap"] = self.overlap
         return self.tuned
 
     def step(self, gb, eye, variant=0, events=None):
