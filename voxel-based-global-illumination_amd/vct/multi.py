@@ -251,10 +251,12 @@ class FrameTracer:
         self.gather()
         return self.diff, self.spec
 
+    tune_pairs = 3        # normal-priority stream pairs tune() tries (plus one high-priority pair)
+
     def tune(self, gb, eye, variant=0, frames=16, gain=1.015, warm=8):
-        """Times `frames` pipelined frames on one stream and as many overlapped on each of two
-        stream pairs (normal and high priority; after `warm` untimed frames each: the first
-        launches on a fresh stream pay a one-time cost), keeps the
+        """Times `frames` pipelined frames on one stream and as many overlapped on each of
+        `tune_pairs` normal stream pairs and one high-priority pair (after `warm` untimed
+        frames each: the first launches on a fresh stream pay a one-time cost), keeps the
         fastest overlap if it is `gain` times faster than one stream; returns the ms / frame.
         Which hardware queues a pair lands on matters (measured on one MI355X, 1080p: one
         normal pair 1.21 ms, another 1.11, a high-priority pair 1.12, one stream 1.17), hence
@@ -265,8 +267,10 @@ class FrameTracer:
             return None
         self.auto = False                             # step() below runs the chosen mode
         main = t.cuda.current_stream(self.device)
-        pairs = {"one stream": None, "two streams": self.streams,
-                 "two high-priority streams": [t.cuda.Stream(self.device, priority=-1) for _ in range(2)]}
+        pairs = {"one stream": None, "two streams": self.streams}
+        for i in range(1, self.tune_pairs):
+            pairs[f"two streams ({i + 1})"] = [t.cuda.Stream(self.device) for _ in range(2)]
+        pairs["two high-priority streams"] = [t.cuda.Stream(self.device, priority=-1) for _ in range(2)]
         ms = {}
         for name, pair in pairs.items():
             self.drain()
@@ -284,10 +288,10 @@ class FrameTracer:
             e1.record(main)
             e1.synchronize()
             ms[name] = e0.elapsed_time(e1) / frames
-        best = min(("two streams", "two high-priority streams"), key=lambda k: ms[k])
+        best = min((k for k in pairs if pairs[k] is not None), key=lambda k: ms[k])
         self.overlap = ms[best] * gain < ms["one stream"]
         self.streams = pairs[best]
-        self.tuned = {k.replace(" ", "_").replace("-", "_") + "_ms": round(v, 4) for k, v in ms.items()}
+        self.tuned = {"ms": {k: round(v, 4) for k, v in ms.items()}}
         self.tuned["chosen"] = best if self.overlap else "one stream"
         self.tuned["overlap"] = self.overlap
         return self.tuned
