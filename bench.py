@@ -642,7 +642,7 @@ def frame_loop(torch, ctx, gb, w, h, eye, stream, frames, variant=0):
     """A renderer's steady state: `frames` default-variant frames on one G-buffer after
     the context's choice for it has settled.  Per frame: the K4 time on the stream
     (events) and the host time of the trace call (a launch path that blocked on the GPU
-    would show here).  The tuner watches every 16th launch without blocking and times
+    would show here).  The tuner watches every 2nd launch without blocking and times
     again only on a drift (vct_trace_form), so max / median stays near 1."""
     import numpy as np
     d, sp = torch.empty((h, w, 4), device=gb[0].device), torch.empty((h, w, 4), device=gb[0].device)
