@@ -210,17 +210,7 @@ class FrameTracer:
                 return [w] if async_op else []
             d.all_gather(list(self.gath[buf].unbind(0)), self.comp[buf])   # gloo (CPU rehearsal)
             return []
-        tpx = TILE * TILE
-        ops = []
-        if self.rank == self.root:
-            for r in range(self.world):
-                nt = tiles_for_rank(self.w, self.h, r, self.world)
-                if r == self.root or nt == 0:
-                    continue
-                off = 2 * tile_offset(self.w, self.h, r, self.world) * tpx
-                ops.append(d.P2POp(d.irecv, self.gath[buf][off:off + 2 * nt * tpx], r))
-        elif self.my_tiles:
-            ops.append(d.P2POp(d.isend, self.comp[buf].view(-1, 4), self.root))
+        ops = self._p2p_ops(buf)
         if not ops:
             return []
         works = d.batch_isend_irecv(ops)
@@ -229,6 +219,26 @@ class FrameTracer:
                 w.wait()
             return []
         return works
+
+    def _p2p_ops(self, buf):
+        """The "present" exchange of buffer set `buf` as P2P op descriptors, built once per
+        set (the root's receive list is the per-frame host cost that grows with the ranks)."""
+        if not hasattr(self, "_ops"):
+            self._ops = {}
+        if buf not in self._ops:
+            d, tpx = self.dist, TILE * TILE
+            ops = []
+            if self.rank == self.root:
+                for r in range(self.world):
+                    nt = tiles_for_rank(self.w, self.h, r, self.world)
+                    if r == self.root or nt == 0:
+                        continue
+                    off = 2 * tile_offset(self.w, self.h, r, self.world) * tpx
+                    ops.append(d.P2POp(d.irecv, self.gath[buf][off:off + 2 * nt * tpx], r))
+            elif self.my_tiles:
+                ops.append(d.P2POp(d.isend, self.comp[buf].view(-1, 4), self.root))
+            self._ops[buf] = ops
+        return self._ops[buf]
 
     def _untile(self, buf):
         if self.world == 1:
