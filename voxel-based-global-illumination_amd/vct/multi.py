@@ -170,10 +170,28 @@ class FrameTracer:
         # one rank: the frames themselves alternate (the trace writes them)
         self.outs = [(torch.zeros((h, w, 4), dtype=f32, device=device),
                       torch.zeros((h, w, 4), dtype=f32, device=device)) for _ in range(nsets if world == 1 else 1)]
-        self.diff, self.spec = self.outs[0]
+        self._set = 0            # the set holding the latest retired frame (one rank)
+        self._ready = None       # its completion event, waited for when it is read (one rank, overlap)
         self.nsets = nsets
         self.cur = 0
         self.pending = None
+
+    def _order_reads(self):
+        if self._ready is not None:
+            self.torch.cuda.current_stream(self.device).wait_event(self._ready)
+            self._ready = None
+
+    @property
+    def diff(self):
+        """Diffuse + AO of the latest completed frame, ordered on the caller's current stream."""
+        self._order_reads()
+        return self.outs[self._set if self.world == 1 else 0][0]
+
+    @property
+    def spec(self):
+        """Specular of the latest completed frame, ordered on the caller's current stream."""
+        self._order_reads()
+        return self.outs[self._set if self.world == 1 else 0][1]
 
     @property
     def holds_frame(self) -> bool:
@@ -242,7 +260,7 @@ class FrameTracer:
 
     def _untile(self, buf):
         if self.world == 1:
-            self.diff, self.spec = self.outs[buf]
+            self._set = buf
         elif self.mode == "allgather":
             self.ctx.untile_planes_device(self.gath[buf], self.w, self.h, self.world, (self.diff, self.spec))
         elif self.rank == self.root:
@@ -342,19 +360,39 @@ class FrameTracer:
         finally:
             if ts is not None:
                 self.ctx.set_stream(saved)
-        self.drain()
+        self._retire(lazy=True)
         self.pending = (works, b, ts)
 
+    def _retire(self, lazy):
+        """Completes the pending frame.  Several ranks: the caller's stream waits for its
+        exchange and un-permutes it.  One rank with overlap and `lazy`: nothing is queued on
+        the caller's stream (a wait there, every frame, would hold up whatever trace stream
+        shares its hardware queue); the frame's completion event is waited for when `diff` /
+        `spec` are read."""
+        if self.pending is None:
+            return
+        works, b, ts = self.pending
+        self.pending = None
+        cur = self.torch.cuda.current_stream(self.device)
+        for w in works:
+            w.wait()                                        # current stream waits for the exchange
+        self._ready = None
+        if ts is not None:
+            if lazy and self.world == 1:
+                self._ready = self.torch.cuda.Event()
+                self._ready.record(ts)
+            else:
+                cur.wait_stream(ts)
+        self._untile(b)
+
     def drain(self):
-        """Completes the pending frame on the caller's current stream."""
-        if self.pending is not None:
-            works, b, ts = self.pending
-            self.pending = None
-            for w in works:
-                w.wait()                                    # current stream waits for the exchange
-            if ts is not None:
-                self.torch.cuda.current_stream(self.device).wait_stream(ts)
-            self._untile(b)
+        """Completes the pending frame and orders the caller's current stream after every
+        frame traced so far."""
+        self._retire(lazy=False)
+        if self.overlap and self.streams is not None:
+            cur = self.torch.cuda.current_stream(self.device)
+            for st in self.streams:
+                cur.wait_stream(st)
 
 
 class _Null:
