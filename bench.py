@@ -668,8 +668,12 @@ def frame_loop(torch, ctx, gb, w, h, eye, stream, frames, variant=0):
     ms = np.array([a.elapsed_time(b) for a, b in ev])
     med = float(np.median(ms))
     return {"frames": frames, "settled_form": form_name(settled), "k4_ms_median": round(med, 4),
-            "k4_ms_p99": round(float(np.percentile(ms, 99)), 4), "k4_ms_max": round(float(ms.max()), 4),
+            "k4_ms_p99": round(float(np.percentile(ms, 99)), 4),
+            "k4_ms_p999": round(float(np.percentile(ms, 99.9)), 4), "k4_ms_max": round(float(ms.max()), 4),
             "max_over_median": round(float(ms.max()) / med, 3),
+            # isolated spikes (a single slow frame in 5 000 with no tuner activity: the tuner
+            # logs every re-timing under VCT_TUNE_LOG) show up here as a count of 1-2
+            "frames_over_1p5x_median": int((ms > 1.5 * med).sum()),
             "host_launch_ms_median": round(float(np.median(host)) * 1e3, 4),
             "host_launch_ms_max": round(float(host.max()) * 1e3, 4), "wall_ms_per_frame": round(wall / frames * 1e3, 4),
             "forms_seen": sorted(form_name(f) or "timing" for f in forms)}
