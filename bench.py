@@ -19,12 +19,14 @@ tiles are split).  Frames are pipelined as a renderer's frame loop runs them
 f+1, and frame f may be traced on trace stream f % 2, so that the next frame's
 trace fills the tail of the previous K4 launch -- FrameTracer.tune times both
 before the warmup and keeps the faster (`overlap_tune`; `--overlap on|off`
-forces it); every
-timed step still traces, exchanges and un-permutes one whole frame, and the
-pipeline is drained inside the timed region.  The roofline's K4 launch
-duration (`k4_kernel_ms_avg`) is timed after the loop with K frames back to
-back on one stream (the kernel alone); `k4_kernel_ms_avg_overlapped` is the
-launches' average inside the pipelined loop, where two traces share the chip.  The level-0 grid is injected
+forces it); every timed step still traces, exchanges and un-permutes one
+whole frame, and the pipeline is drained inside the timed region.  The
+roofline's K4 launch duration (`k4_kernel_ms_avg`) is timed after the loop
+with K frames back to back on one stream (the kernel alone; rocprofv3 agrees
+with it on a `--overlap off` run, profiles/r03_r3f_*); `k4_kernel_ms_avg_overlapped`
+is the launches' start-to-end average inside the pipelined loop, where two
+traces share the chip, and `roofline.pipelined` the same per-launch work over
+the timed loop's time per frame.  The level-0 grid is injected
 on rank 0 and broadcast (RCCL) before the timed region, as when the light
 changes; every other rank also injects it itself (the replicated alternative,
 checked bit-equal); K1/K2/K3, the broadcast, the trace alone (slowest rank) and
@@ -859,6 +861,14 @@ def run(args, world):
     key = profile_key(n, w, h, args.scene, args.gbuffer, args.n_diffuse, spec, args.variant, world)
     rec, reason = load_profile(args.profile_json, key)
     roof = roofline(rec, reason, m["k4_kernel_ms_avg"], m["local_texels"], m["local_valid"], args.profile_json, key)
+    if roof.get("frac") is not None and m["ms_per_step"] > 0:
+        # the same per-launch work over the pipelined frame time: with frame overlap a launch's
+        # own start-to-end time includes the other frame's share of the chip, so the rate the
+        # timed loop sustains is work per frame / ms per step
+        r_ = roof["frac"] * m["k4_kernel_ms_avg"] / m["ms_per_step"]
+        roof["pipelined"] = {"achieved": round(roof["achieved"] * m["k4_kernel_ms_avg"] / m["ms_per_step"], 1),
+                             "frac": round(r_, 4), "ms_per_frame": round(m["ms_per_step"], 4),
+                             "basis": "per-launch counts / (timed wall time / K)"}
 
     result = None
     if rank == 0:
