@@ -205,6 +205,7 @@ struct BlockK {
     float4* pyr;
     uint64_t off[kMaxLevels + 1];             // float4 offset of each level
     int n, l;                                 // grid edge, first level built
+    int brick_writes;                         // level l stored in brick order from LDS (VCT_K3_WRITE)
 };
 
 template <int MODE>
@@ -251,9 +252,26 @@ __global__ void __launch_bounds__(kBlkT) k3_block(const BlockK k) {
         else out[0] = box_of(ch);
     }
     __syncthreads();                          // every staged brick has been read
-    if (t < E3) {
+    const size_t vl = (size_t)nl * nl * nl;
+    if (E == kBlk && k.brick_writes) {
+        // results to LDS first; then thread t writes texel t of the block in brick order
+        // (bricks of 2^3 parents, 4 per row: a wave stores two 512-B runs per face)
+        if (t < E3) {
+#pragma unroll
+            for (int f = 0; f < FACES; ++f) st[f * E3 + t] = out[f];
+        }
+        __syncthreads();
+        const int q = t >> 3, j = t & 7;
+        const int bx = q & 3, by = (q >> 2) & 3, bz = q >> 4;
+        const int lin = (2 * bx + (j & 1)) + kBlk * ((2 * by + ((j >> 1) & 1)) + kBlk * (2 * bz + (j >> 2)));
+        const uint32_t nb = nl >> 1;
+        const size_t brick = (size_t)((X0 >> 1) + (uint32_t)bx) +
+                             (size_t)nb * ((size_t)((Y0 >> 1) + (uint32_t)by) + (size_t)nb * ((Z0 >> 1) + (uint32_t)bz));
+#pragma unroll
+        for (int f = 0; f < FACES; ++f) k.pyr[k.off[k.l] + (size_t)(f0 + f) * vl + brick * 8 + (size_t)j] = st[f * E3 + lin];
+    } else if (t < E3) {
         const uint32_t x = X0 + (uint32_t)(t % E), y = Y0 + (uint32_t)((t / E) % E), z = Z0 + (uint32_t)(t / (E * E));
-        const size_t vl = (size_t)nl * nl * nl, ti = texel_index(x, y, z, nl);
+        const size_t ti = texel_index(x, y, z, nl);
 #pragma unroll
         for (int f = 0; f < FACES; ++f) {
             st[f * E3 + t] = out[f];
@@ -326,6 +344,14 @@ hipError_t launch_mips(vct_ctx* c) {
     k.pyr = g.pyr;
     for (int i = 0; i <= kMaxLevels; ++i) k.off[i] = g.lvl_off[i];
     k.n = (int)g.n;
+    // level l of a full 8^3 block goes out in brick order from LDS: whole 512-B runs per
+    // wave instead of 64-B half bricks (256^3: 0.126 -> 0.122 ms, 512^3: 0.890 -> 0.857 ms);
+    // VCT_K3_WRITE=0 writes each parent from its thread (A/B)
+    static const int bw = [] {
+        const char* v = getenv("VCT_K3_WRITE");
+        return v ? atoi(v) : 1;
+    }();
+    k.brick_writes = bw;
     for (uint32_t l = 1; l <= g.L;) {
         const uint32_t nl = g.n >> l, E = nl < (uint32_t)kBlk ? nl : (uint32_t)kBlk;
         const uint32_t nbk = nl / E, blocks = nbk * nbk * nbk;
