@@ -366,6 +366,28 @@ def progress(rank, what):
         print(f"[bench {time.perf_counter() - _T0:7.1f} s] {what}", file=sys.stderr, flush=True)
 
 
+_JSON_FD = None
+
+
+def protect_stdout():
+    """The JSON line is the only thing on stdout: native libraries of a rank (gloo's
+    connection message, RCCL) print to fd 1 too, so fd 1 becomes stderr and the line
+    goes to the saved descriptor."""
+    global _JSON_FD
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit(obj):
+    line = json.dumps(obj) + "\n"
+    if _JSON_FD is None:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line.encode())
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "0") or 0)
@@ -375,6 +397,7 @@ def main():
         world = 1
     if args.gpus != world:
         raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE is {world}: one process per GPU")
+    protect_stdout()
     if args.dry_run:
         return dry_run(args, world)
     run(args, world)
@@ -409,7 +432,7 @@ def dry_run(args, world):
         ok = max_over_ranks(torch, dist, dev, [0.0 if ok else 1.0], world)[0] == 0.0
         res[mode] = {"frame_ok": ok, "ms_per_step": round(el / args.steps * 1e3, 3)}
     if rank == 0:
-        print(json.dumps({
+        emit({
             "metric": METRIC, "value": None, "unit": "Mcone-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "dry run (CPU, gloo, pattern stand-in trace)",
@@ -417,7 +440,7 @@ def dry_run(args, world):
             "config": {"workload": "rank plumbing only", "width": w, "height": h,
                        "parallelism": f"screen-tiles x{world}"},
             "trace_ms_max_rank": None, "gather_ms": None, "allgather_ms": None,
-        }), flush=True)
+        })
     if world > 1:
         dist.destroy_process_group()
 
@@ -968,7 +991,7 @@ def run(args, world):
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
 
 
 if __name__ == "__main__":
