@@ -175,6 +175,7 @@ class FrameTracer:
         self.nsets = nsets
         self.cur = 0
         self.pending = None
+        self._ops = {}           # "present" P2P descriptors per buffer set (_p2p_ops)
 
     def _order_reads(self):
         if self._ready is not None:
@@ -241,8 +242,6 @@ class FrameTracer:
     def _p2p_ops(self, buf):
         """The "present" exchange of buffer set `buf` as P2P op descriptors, built once per
         set (the root's receive list is the per-frame host cost that grows with the ranks)."""
-        if not hasattr(self, "_ops"):
-            self._ops = {}
         if buf not in self._ops:
             d, tpx = self.dist, TILE * TILE
             ops = []
