@@ -278,7 +278,7 @@ class FrameTracer:
         self.gather()
         return self.diff, self.spec
 
-    tune_pairs = 3        # normal-priority stream pairs tune() tries (plus one high-priority pair)
+    tune_pairs = 4        # normal-priority stream pairs tune() tries (plus one high-priority pair)
 
     def tune(self, gb, eye, variant=0, frames=16, gain=1.015, warm=8):
         """Times `frames` pipelined frames on one stream and as many overlapped on each of
