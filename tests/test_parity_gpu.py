@@ -976,6 +976,38 @@ def test_reorder_equals_screen_order(gpu_ready, kind):
 
 
 @pytest.mark.gpu
+def test_reordered_frames_overlapped(gpu_ready):
+    """Consecutive ray-reordered frames (variant 0x8000: key kernel, radix sort, K4) traced
+    concurrently on two streams (FrameTracer overlap): each stream has its own key / sort
+    scratch, so every frame equals its single-stream trace bit for bit."""
+    import torch
+    from vct import scenes
+    from vct.multi import FrameTracer
+    n, w, h = 32, 320, 200
+    ctx, s, arrs, (g0, E) = gpu_pipeline(n, "atrium")
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ao, nm = ctx.download_voxels()
+    gb = tuple(torch.from_numpy(x).to(dev) for x in scenes.gbuffer_rand(ao, nm, g0, E, w, h, seed=7))
+    eyes = [[0.05 * f, 0.0, 3.0] for f in range(6)]
+    refs = []
+    for e in eyes:
+        d, sp = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+        ctx.trace_device(*gb, w, h, e, d, sp, variant=0x8000)
+        refs.append((d, sp))
+    tr = FrameTracer(ctx, torch, None, w, h, 0, 1, dev, overlap=True)
+    for f, e in enumerate(eyes):
+        tr.step(gb, e, variant=0x8000)
+        if f >= 1:
+            torch.cuda.synchronize()
+            assert torch.equal(tr.diff, refs[f - 1][0]) and torch.equal(tr.spec, refs[f - 1][1]), f
+    tr.drain()
+    torch.cuda.synchronize()
+    assert torch.equal(tr.diff, refs[-1][0]) and torch.equal(tr.spec, refs[-1][1])
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_trace_form_tuner(gpu_ready):
     """The default variant times its two compiled forms on the first counter-free launches
     of a workload and keeps the faster one (vct_trace_form): every launch, whichever form
