@@ -943,7 +943,17 @@ def run(args, world):
     capi = None
     if world > 1:
         if os.environ.get("VCT_DIST_BACKEND", "nccl") == "nccl":
-            capi = capi_leg(args, torch, dist, ctx, rank, world, dev, stream, m["_gb"], m["_eye"])
+            # a failure on any rank (the C-ABI returns VCT_ECOMM after its deadline and aborts
+            # its communicator) is recorded, agreed on over the torch group, and the line goes on
+            err = None
+            try:
+                capi = capi_leg(args, torch, dist, ctx, rank, world, dev, stream, m["_gb"], m["_eye"])
+            except Exception as e:   # noqa: BLE001 -- reported in the JSON line
+                err = f"{type(e).__name__}: {e}"[:300]
+                capi = None
+            if max_over_ranks(torch, dist, dev, [0.0 if err is None else 1.0], world)[0] != 0.0:
+                capi = {"error": err or "failed on another rank", "present_equal": None, "allgather_equal": None,
+                        "bcast_equal": None}
         else:
             capi = {"note": "skipped: the C-ABI RCCL path needs one GPU per rank (VCT_DIST_BACKEND is not nccl)",
                     "present_equal": None, "allgather_equal": None, "bcast_equal": None,
