@@ -38,9 +38,9 @@ def test_voxelize_inject_mips_bitexact(gpu_ready, oracle_mod, name, n):
 @pytest.mark.parametrize("aniso", [True, False])
 @pytest.mark.parametrize("n", [4, 8, 32, 64, 128])
 def test_mips_bitexact_random_level0(gpu_ready, oracle_mod, aniso, n):
-    """K3 on random level 0: every size path of the launch plan (n = 4, 8: the fused tail
-    only; 32: one tail block per face; 64, 128: several tail blocks and the last-block
-    ticket), built twice (the per-face tickets reset) -- bit-exact vs the oracle."""
+    """K3 on random level 0: every size path of the launch plan (n = 4, 8: blocks smaller
+    than 8 x 8 x 4 parents; 32..128: full blocks, then a short top launch), built twice --
+    bit-exact vs the oracle."""
     from vct import Context
     rng = np.random.default_rng(3 + n)
     a = (rng.random((n, n, n)) < 0.3).astype(np.float32)
@@ -52,6 +52,42 @@ def test_mips_bitexact_random_level0(gpu_ready, oracle_mod, aniso, n):
         ctx.build_mips()
         assert np.array_equal(gpu_pyramid_flat(ctx), ref)
     ctx.close()
+
+
+@pytest.mark.parametrize("plan", [{"VCT_K3_BZ": "8"}, {"VCT_K3_BZ": "2"}, {"VCT_K3_PLAN": "level"}],
+                         ids=["block8", "block2", "per-level"])
+def test_mips_alternate_plans_bitexact(gpu_ready, oracle_mod, tmp_path, plan):
+    """The K3 launch plans kept for A/B (8^3 and 8x8x2 parent blocks, per-level kernels;
+    chosen once per process from the environment) build the same pyramid as the oracle:
+    a child process builds random level 0s at every size path, the parent compares."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cases = [(n, aniso) for n in (4, 16, 64, 128) for aniso in (True, False)]
+    ins = {}
+    for n, aniso in cases:
+        rng = np.random.default_rng(11 + n)
+        a = (rng.random((n, n, n)) < 0.3).astype(np.float32)
+        ins[f"r{n}"] = np.concatenate([rng.random((n, n, n, 3)).astype(np.float32) * a[..., None], a[..., None]], -1)
+    np.savez(str(tmp_path / "in.npz"), **ins)
+    child = (
+        "import sys, numpy as np\n"
+        f"sys.path[:0] = [{repo!r}, {os.path.join(repo, 'tests')!r}, "
+        f"{os.path.join(repo, 'voxel-based-global-illumination_amd')!r}]\n"
+        "from vct import Context\n"
+        "from helpers import gpu_pyramid_flat\n"
+        f"d = np.load({str(tmp_path / 'in.npz')!r}); out = {{}}\n"
+        f"for n, aniso in {cases!r}:\n"
+        "    c = Context(n, (0, 0, 0), 1.0, aniso=aniso); c.upload_level0(d[f'r{n}'])\n"
+        "    c.build_mips(); out[f'p{n}_{int(aniso)}'] = gpu_pyramid_flat(c); c.close()\n"
+        f"np.savez({str(tmp_path / 'out.npz')!r}, **out)\n")
+    p = subprocess.run([sys.executable, "-c", child], env={**os.environ, **plan}, capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stderr
+    out = np.load(str(tmp_path / "out.npz"))
+    for n, aniso in cases:
+        assert np.array_equal(out[f"p{n}_{int(aniso)}"], oracle_mod.build_mips(n, ins[f"r{n}"], aniso)), (n, aniso)
 
 
 def test_mips_constant_kat_gpu(gpu_ready):

@@ -199,7 +199,6 @@ __global__ void __launch_bounds__(256) k3_levelN(const float4* __restrict__ src,
 // in the same array, each level's results (linear, x fastest) for the next one.
 enum { kIso6 = 0, kFace = 1, kBox = 2 };
 constexpr int kBlk = 8;                       // block edge (parents of level l)
-constexpr int kBlkT = kBlk * kBlk * kBlk;     // threads of a workgroup
 
 struct BlockK {
     float4* pyr;
@@ -208,27 +207,29 @@ struct BlockK {
     int brick_writes;                         // level l stored in brick order from LDS (VCT_K3_WRITE)
 };
 
-template <int MODE>
-__global__ void __launch_bounds__(kBlkT) k3_block(const BlockK k) {
-    __shared__ float4 st[kBlkT * 9];
+template <int MODE, int BZ>
+__global__ void __launch_bounds__(kBlk * kBlk * BZ) k3_block(const BlockK k) {
+    constexpr int kT = kBlk * kBlk * BZ;      // threads: one per parent of a full block
+    __shared__ float4 st[kT * 9];
     constexpr int FACES = MODE == kIso6 ? 6 : 1;
     const int t = (int)threadIdx.x;
     const int f0 = MODE == kFace ? (int)blockIdx.y : 0;
     const uint32_t nl = (uint32_t)k.n >> k.l, nc = 2u * nl;
-    const int E = nl < (uint32_t)kBlk ? (int)nl : kBlk, E3 = E * E * E;
+    // block of E x E x Ez parents (E = min(8, n_l), Ez = min(BZ, n_l))
+    const int E = nl < (uint32_t)kBlk ? (int)nl : kBlk, Ez = nl < (uint32_t)BZ ? (int)nl : BZ, E3 = E * E * Ez;
     const uint32_t nbk = nl / (uint32_t)E, b = blockIdx.x;
-    const uint32_t X0 = (b % nbk) * E, Y0 = ((b / nbk) % nbk) * E, Z0 = (b / (nbk * nbk)) * E;
+    const uint32_t X0 = (b % nbk) * E, Y0 = ((b / nbk) % nbk) * E, Z0 = (b / (nbk * nbk)) * Ez;
     // children: face f0 of level l-1 (level 0 for kIso6 and level 1 of kBox)
     const float4* src = k.pyr + k.off[k.l - 1] + (MODE == kFace ? (size_t)f0 * nc * nc * nc : 0);
     // staging: float4 u = 8 c + j of the block's child bricks (c linear over the block's
     // parents, x fastest; the child brick of parent (x, y, z) is brick x + nl (y + nl z))
     {
-        // (u < E3 * 8 always holds for E = 8; a smaller block clamps its spare loads)
+        // (u < E3 * 8 always holds for a full block; a smaller one clamps its spare loads)
         float4 r[8];
         const int lim = E3 * 8 - 1;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int u = min(i * kBlkT + t, lim);
+            const int u = min(i * kT + t, lim);
             const int c = u >> 3, j = u & 7;
             const uint32_t cx = (uint32_t)(c % E), cy = (uint32_t)((c / E) % E), cz = (uint32_t)(c / (E * E));
             const size_t brick = (size_t)(X0 + cx) + (size_t)nl * ((size_t)(Y0 + cy) + (size_t)nl * (Z0 + cz));
@@ -236,7 +237,7 @@ __global__ void __launch_bounds__(kBlkT) k3_block(const BlockK k) {
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int u = i * kBlkT + t;
+            const int u = i * kT + t;
             if (u <= lim) st[(u >> 3) * 9 + (u & 7)] = r[i];
         }
     }
@@ -253,7 +254,7 @@ __global__ void __launch_bounds__(kBlkT) k3_block(const BlockK k) {
     }
     __syncthreads();                          // every staged brick has been read
     const size_t vl = (size_t)nl * nl * nl;
-    if (E == kBlk && k.brick_writes) {
+    if (E == kBlk && Ez == BZ && k.brick_writes) {
         // results to LDS first; then thread t writes texel t of the block in brick order
         // (bricks of 2^3 parents, 4 per row: a wave stores two 512-B runs per face)
         if (t < E3) {
@@ -279,16 +280,17 @@ __global__ void __launch_bounds__(kBlkT) k3_block(const BlockK k) {
         }
     }
     __syncthreads();
-    // levels l+1 ..: from the previous level's results in LDS (face-major, linear)
-    int base = 0, Ein = E, l = k.l;
-    for (int Eo = E >> 1; Eo >= 1; Eo >>= 1) {
+    // levels l+1 ..: from the previous level's results in LDS (face-major, linear), while
+    // every block edge still halves (log2 Ez levels)
+    int base = 0, Ein = E, Ezin = Ez, l = k.l;
+    for (int Eo = E >> 1, Ezo = Ez >> 1; Ezo >= 1; Eo >>= 1, Ezo >>= 1) {
         ++l;
-        const int cnt = Eo * Eo * Eo, nb = base + FACES * Ein * Ein * Ein;
+        const int cnt = Eo * Eo * Ezo, nin = Ein * Ein * Ezin, nb = base + FACES * nin;
         const uint32_t no = (uint32_t)k.n >> l;
         if (t < FACES * cnt) {
             const int f = t / cnt, q = t % cnt;
             const int qx = q % Eo, qy = (q / Eo) % Eo, qz = q / (Eo * Eo);
-            const float4* cin = st + base + f * Ein * Ein * Ein;
+            const float4* cin = st + base + f * nin;
             float4 ch[2][2][2];
 #pragma unroll
             for (int dz = 0; dz < 2; ++dz)
@@ -306,6 +308,7 @@ __global__ void __launch_bounds__(kBlkT) k3_block(const BlockK k) {
         __syncthreads();
         base = nb;
         Ein = Eo;
+        Ezin = Ezo;
     }
 }
 
@@ -352,17 +355,33 @@ hipError_t launch_mips(vct_ctx* c) {
         return v ? atoi(v) : 1;
     }();
     k.brick_writes = bw;
+    // block depth: 8 x 8 x 4 parents (256 threads, 36 KB of LDS, subtrees three levels
+    // deep) beat the 8^3 cube (512 threads, 72 KB, four levels) by 4 % at 256^3 and 9 % at
+    // 512^3, and 8 x 8 x 2 by 3-4 %: twice the workgroups in flight per CU hide the staging
+    // loads better than the one saved launch. VCT_K3_BZ = 8 | 2 selects the others (A/B).
+    static const int bz = [] {
+        const char* v = getenv("VCT_K3_BZ");
+        const int b = v ? atoi(v) : 4;
+        return b == 8 || b == 2 ? b : 4;
+    }();
     for (uint32_t l = 1; l <= g.L;) {
         const uint32_t nl = g.n >> l, E = nl < (uint32_t)kBlk ? nl : (uint32_t)kBlk;
-        const uint32_t nbk = nl / E, blocks = nbk * nbk * nbk;
+        const uint32_t Ez = nl < (uint32_t)bz ? nl : (uint32_t)bz;
+        const uint32_t nbk = nl / E, all = nbk * nbk * (nl / Ez);
+        const uint32_t blocks = all;
         k.l = (int)l;
-        if (!g.aniso)
-            hipLaunchKernelGGL(k3_block<kBox>, dim3(blocks), dim3(kBlkT), 0, c->stream, k);
-        else if (l == 1)
-            hipLaunchKernelGGL(k3_block<kIso6>, dim3(blocks), dim3(kBlkT), 0, c->stream, k);
-        else
-            hipLaunchKernelGGL(k3_block<kFace>, dim3(blocks, 6), dim3(kBlkT), 0, c->stream, k);
-        l += (uint32_t)__builtin_ctz(E) + 1u;
+#define VCT_K3_LAUNCH(BZv)                                                                                      \
+    do {                                                                                                        \
+        constexpr uint32_t thr = (uint32_t)(kBlk * kBlk * BZv);                                                \
+        if (!g.aniso) hipLaunchKernelGGL((k3_block<kBox, BZv>), dim3(blocks), dim3(thr), 0, c->stream, k);     \
+        else if (l == 1) hipLaunchKernelGGL((k3_block<kIso6, BZv>), dim3(blocks), dim3(thr), 0, c->stream, k); \
+        else hipLaunchKernelGGL((k3_block<kFace, BZv>), dim3(blocks, 6), dim3(thr), 0, c->stream, k);          \
+    } while (0)
+        if (bz == 8) VCT_K3_LAUNCH(8);
+        else if (bz == 2) VCT_K3_LAUNCH(2);
+        else VCT_K3_LAUNCH(4);
+#undef VCT_K3_LAUNCH
+        l += (uint32_t)__builtin_ctz(Ez) + 1u;
     }
     return hipGetLastError();
 }
