@@ -164,6 +164,46 @@ def test_trace_parity(gpu_ready, oracle_mod, name, n, kind, aniso, nd, spec):
     ctx.close()
 
 
+@pytest.mark.parametrize("kind", ["scene", "jitter"])
+def test_occupancy_form_curved_bitexact(gpu_ready, oracle_mod, kind):
+    """Curved surfaces in the occupancy form: cones whose valid lanes select four faces
+    stage 4 x 4 x 3 bricks (four 54-slot face blocks) instead of gathering per lane;
+    the courtyard's columns and the jittered normals make many such waves.  Forced
+    occupancy form, screen order and reordered, with and without counters: bit-exact."""
+    import torch
+    from vct import scenes
+    from vct.camera import Camera
+    n, w, h = 64, 192, 128
+    ctx, s, arrs, (g0, E) = gpu_pipeline(n, "courtyard")
+    dev = torch.device("cuda")
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    cam = Camera()
+    gb = [torch.empty((h, w, 4), device=dev) for _ in range(3)]
+    ctx.gbuffer_raster_device(cam, w, h, scenes.ROUGHNESS, *gb)       # the raster (1 M triangles)
+    torch.cuda.synchronize()
+    pos, nrm, alb = (g.cpu().numpy() for g in gb)
+    assert (pos[..., 3] != 0).mean() > 0.5
+    if kind == "jitter":
+        rng = np.random.default_rng(9)
+        nv = np.stack([rng.uniform(-0.05, 0.05, (h, w)), np.full((h, w), 0.9), np.full((h, w), 0.4)], -1)
+        nv /= np.linalg.norm(nv, axis=-1, keepdims=True)
+        nrm = nrm.copy()
+        nrm[..., :3] = np.where(pos[..., 3:4] != 0, nv, nrm[..., :3]).astype(np.float32)
+        gb[1] = torch.from_numpy(nrm).to(dev)
+    ref = oracle_mod.trace(n, g0, E, ctx.download_level(0), gpu_pyramid_flat(ctx), pos, nrm, alb, cam.position)
+    for variant, counted in ((0x6000000, True), (0x2008000, True), (0x6000000, False), (0x2008000, False)):
+        d = torch.full((h, w, 4), -1.0, device=dev)
+        sp = torch.full((h, w, 4), -1.0, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        ctx.trace_device(*gb, w, h, cam.position, d, sp, cone_steps=cnt if counted else None, variant=variant)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), ref["diffuse"]), f"variant {variant:#x} diffuse"
+        assert np.array_equal(sp.cpu().numpy(), ref["spec"]), f"variant {variant:#x} spec"
+        if counted:
+            assert int(cnt[0]) == ref["cone_steps"]
+    ctx.close()
+
+
 @pytest.mark.parametrize("kind", ["scene", "rand", "mirror", "jitter"])
 def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
     """The K4 variants (0 = LDS bricks, 1 = per-lane gathers, 2 = bricks without

@@ -513,6 +513,12 @@ __device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, f
 // every z step onto the same banks.
 constexpr int kBz = 19;
 constexpr int kBlk = 3 * kBz + 16;              // one face block: 73 slots
+// four-face cones in the occupancy form (VCT_K4_F43): 4 x 4 x 3 bricks, four 54-slot
+// face blocks (216 slots) in the 219-slot entry
+#ifndef VCT_K4_F43
+#define VCT_K4_F43 1
+#endif
+constexpr int kBlk3 = 2 * kBz + 16;
 // float4 slots per cache entry: up to 4 face blocks (3 without the four-face union)
 // The two cache entries live in LDS regions 0 and 1 (entry a in region `flip`): 9344 B
 // per wave with the union (4 waves/SIMD fit the 160 KB), 7008 B without (5 waves/SIMD).
@@ -539,6 +545,8 @@ struct ConeCtl {                 // wave-uniform facts about one cone
     bool dir_uniform;            // every valid lane has the same wd = d^2 (bitwise) and the same faces
     int neg;                     // bit a: every valid lane moves toward -axis a (brick slack goes there)
     float uwx, uwy, uwz;         // that wd
+    int z3;                      // 1: faces-mode bricks are 4 x 4 x 3 (a four-face cone in the occupancy form)
+    int bstr;                    // faces-mode block stride (kBlk, or kBlk3 with z3)
 };
 
 struct BrickEntry {
@@ -571,8 +579,9 @@ __device__ __forceinline__ Corner level_corner(int l, float qx, float qy, float 
     return c;
 }
 
-__device__ __forceinline__ bool in_brick(const Corner& c, const BrickEntry& b) {
-    return max(max((uint32_t)(c.ix - b.ox), (uint32_t)(c.iy - b.oy)), (uint32_t)(c.iz - b.oz)) <= 2u;
+// z3 = 1: a 4 x 4 x 3 brick (iz - oz <= 1; the shift keeps a negative offset out of range)
+__device__ __forceinline__ bool in_brick(const Corner& c, const BrickEntry& b, int z3) {
+    return max(max((uint32_t)(c.ix - b.ox), (uint32_t)(c.iy - b.oy)), (uint32_t)(c.iz - b.oz) << z3) <= 2u;
 }
 
 // Brick origin on one axis without a 64-lane reduction: relative to the first
@@ -591,23 +600,23 @@ __device__ __forceinline__ int s_nonzero(unsigned long long m) {
     asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(m) : "scc");
     return r;
 }
-__device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl, int negb) {
+__device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl, int negb, int back = 2) {
     const int b = __builtin_amdgcn_readlane(v, fl);
     const int sg = 1 - 2 * negb;                       // +1 / -1
     const int sv = __mul24(v, sg), sb = b * sg;        // mirrored toward -axis
     const unsigned long long m2 = wballot(sv < sb - 1) & am, m1 = wballot(sv < sb) & am;   // m2 within m1
     const int cnt = s_nonzero(m1) + s_nonzero(m2);
-    return b - sg * cnt - 2 * negb;
+    return b - sg * cnt - back * negb;      // back = brick depth - 2
 }
 
 // a brick origin over the lanes of am (neg: bit a = the cone moves toward -axis a),
 // if every footprint fits the brick there
-__device__ __forceinline__ bool brick_origin(const Corner& c, unsigned long long am, int neg, BrickEntry& b) {
+__device__ __forceinline__ bool brick_origin(const Corner& c, unsigned long long am, int neg, BrickEntry& b, int z3) {
     const int fl = am ? __builtin_ctzll(am) : 0;
     b.ox = wave_origin(c.ix, am, fl, neg & 1);
     b.oy = wave_origin(c.iy, am, fl, (neg >> 1) & 1);
-    b.oz = wave_origin(c.iz, am, fl, (neg >> 2) & 1);
-    return wall_in(am, in_brick(c, b));
+    b.oz = wave_origin(c.iz, am, fl, (neg >> 2) & 1, 2 - z3);
+    return wall_in(am, in_brick(c, b, z3));
 }
 
 enum { kIso = 0, kComb = 1, kFaces = 2 };
@@ -671,6 +680,15 @@ __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const T
         const float4 v = combine3(cc.uwx, cc.uwy, cc.uwz, t.a, t.b, t.c);
         p[0] = v;
         nz = bits4(v);
+    } else if (cc.z3) {             // 4 x 4 x 3: the lanes of z = 3 store nothing
+        nz = 0u;
+        if (lane < 48) {
+            p[0] = t.a;
+            p[kBlk3] = t.b;
+            p[2 * kBlk3] = t.c;
+            p[3 * kBlk3] = t.d;
+            nz = bits4(t.a) | bits4(t.b) | bits4(t.c) | bits4(t.d);
+        }
     } else {
         p[0] = t.a;
         p[kBlk] = t.b;
@@ -751,9 +769,9 @@ struct LaneDir {
     __device__ float wx() const { return dx * dx; }
     __device__ float wy() const { return dy * dy; }
     __device__ float wz() const { return dz * dz; }
-    __device__ int bx() const { return __mul24(kBlk, (int)(blk & 3u)); }
-    __device__ int by() const { return __mul24(kBlk, (int)((blk >> 2) & 3u)); }
-    __device__ int bz() const { return __mul24(kBlk, (int)(blk >> 4)); }
+    __device__ int bx(int str) const { return __mul24(str, (int)(blk & 3u)); }
+    __device__ int by(int str) const { return __mul24(str, (int)((blk >> 2) & 3u)); }
+    __device__ int bz(int str) const { return __mul24(str, (int)(blk >> 4)); }
 };
 
 // One step's blended sample (1 - fr) D_{l0} + fr D_{l0+1} for a wave-uniform l0.
@@ -772,7 +790,9 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const int aniso_mode = cc.dir_uniform ? kComb : kFaces;
     const int modeA = (l0 == 0 || !k.aniso) ? kIso : aniso_mode;
     const int modeB = k.aniso ? aniso_mode : kIso;
-    const bool faces_ok = UNION ? cc.nfaces <= 4 : cc.nfaces == 3;
+    const bool faces_ok = UNION || VCT_K4_F43 ? cc.nfaces <= 4 : cc.nfaces == 3;
+    // faces-mode levels of a four-face cone in the occupancy form: 4 x 4 x 3 bricks
+    const int z3A = modeA == kFaces ? cc.z3 : 0, z3B = modeB == kFaces ? cc.z3 : 0;
     if (bc.a.lvl != l0 && bc.b.lvl == l0) {       // the level advanced by one: b becomes a
         // a cone's level never decreases, so the old a (level l0 - 1) is dead: b moves into
         // a's place, b is emptied and the LDS regions trade roles (no three-way swap)
@@ -786,12 +806,12 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // level A: cached, restaged, or gathered
     const Corner cA = level_corner(l0, qx, qy, qz);
     BrickEntry bA = bc.a;
-    bool useA = bA.lvl == l0 && wall_in(amA, in_brick(cA, bA));
+    bool useA = bA.lvl == l0 && wall_in(amA, in_brick(cA, bA, z3A));
     bool stA = false;
     if (!useA && (modeA != kFaces || faces_okA)) {
         BrickEntry nb{};
         nb.lvl = l0;
-        if (brick_origin(cA, amA, cc.neg, nb)) {
+        if (brick_origin(cA, amA, cc.neg, nb, z3A)) {
             bA = nb;
             bc.a = nb;
             useA = stA = true;
@@ -802,11 +822,11 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     bool useB = false, stB = false;
     if (needB) {
         cB = level_corner(l1, qx, qy, qz);
-        useB = bB.lvl == l1 && wall_in(amB, in_brick(cB, bB));
+        useB = bB.lvl == l1 && wall_in(amB, in_brick(cB, bB, z3B));
         if (!useB && (modeB != kFaces || faces_okB)) {
             BrickEntry nb{};
             nb.lvl = l1;
-            if (brick_origin(cB, amB, cc.neg, nb)) {
+            if (brick_origin(cB, amB, cc.neg, nb, z3B)) {
                 bB = nb;
                 bc.b = nb;
                 useB = stB = true;
@@ -850,11 +870,11 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         // corner-0 texels instead of its own (staged, finite), and its march adds nothing
         // (march_brick scales the sample by 0)
         if (readA)
-            sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA) : 0, modeA != kFaces, ld.bx(), ld.by(), ld.bz(),
+            sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA) : 0, modeA != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr), ld.bz(cc.bstr),
                                   ld.wx(), ld.wy(), ld.wz(), ldsA);
         if (readB)
-            sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB) : 0, modeB != kFaces, ld.bx(), ld.by(),
-                                  ld.bz(), ld.wx(), ld.wy(), ld.wz(), ldsB);
+            sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB) : 0, modeB != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr),
+                                  ld.bz(cc.bstr), ld.wx(), ld.wy(), ld.wz(), ldsB);
         wave_lds_sync();
     }
     pc.mark(3);
@@ -1020,6 +1040,8 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
         // same d^2 everywhere AND one face per axis (d and -d share d^2)
         cc.dir_uniform = wall_in(vm, (wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz)) && cc.nfaces == 3;
+        cc.z3 = !UNION && VCT_K4_F43 && cc.nfaces == 4 ? 1 : 0;
+        cc.bstr = cc.z3 ? kBlk3 : kBlk;
     }
     BrickCache bc;
     bc.a = bc.b = BrickEntry{-1, 0, 0, 0, 0};
