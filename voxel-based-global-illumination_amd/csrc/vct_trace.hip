@@ -36,6 +36,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "vct_internal.h"
 
@@ -125,9 +126,17 @@ __constant__ float c_cones1[1][4] = {VCT_CONES1(VCT_CROW)};
 __constant__ float c_cones9[9][4] = {VCT_CONES9(VCT_CROW)};
 __constant__ float c_cones16[16][4] = {VCT_CONES16(VCT_CROW)};
 
+// level l's buffer range as the O32 kernels bind it (one 16-B scalar load per level view)
+struct LevelRange {
+    const float4* base;          // pyr + lvl_off[l]
+    uint32_t bytes;              // the level's size (every face; num_records is unsigned), 0 above 32 bits
+    uint32_t pad;
+};
+
 struct TraceK {
     const float4* pyr;
     uint64_t lvl_off[kMaxLevels + 1];
+    LevelRange lvl[kMaxLevels + 1];
     int n, L;
     int lgn;                     // log2 n
     float g0x, g0y, g0z, inv_h, tmax;
@@ -247,14 +256,24 @@ struct LevelView<false> {
 // level l (wave-uniform): O32 takes the level's texel offset from the kernel-argument
 // table (one scalar load; measured 0.7-0.9 % faster than deriving it on the scalar unit,
 // which also held ~34 more SGPRs) and its size from shifts (n a power of two)
+// level views from the host's per-level base / size table (1) or derived per view (0)
+#ifndef VCT_K4_LVLTAB
+#define VCT_K4_LVLTAB 1
+#endif
 template <bool O32>
 __device__ __forceinline__ LevelView<O32> level_view(const TraceK& k, int l) {
     if constexpr (O32) {
+#if VCT_K4_LVLTAB
+        // base and size precomputed per level on the host (launch_trace)
+        const LevelRange r = k.lvl[l];
+        return LevelView<true>{__builtin_amdgcn_make_buffer_rsrc((void*)r.base, (short)0, (int)r.bytes, 0x00020000)};
+#else
         const uint32_t lg = (uint32_t)k.lgn, F = k.aniso ? 6u : 1u;
         const uint32_t off = (uint32_t)k.lvl_off[l];   // < 2^31 texels for n <= 512
         const uint32_t bytes = (l == 0 ? 1u : F) << (3u * (lg - (uint32_t)l) + 4u);
         return LevelView<true>{__builtin_amdgcn_make_buffer_rsrc((void*)(k.pyr + off), (short)0, (int)bytes,
                                                                  0x00020000)};
+#endif
     } else {
         return LevelView<false>{k.pyr + k.lvl_off[l]};
     }
@@ -519,6 +538,15 @@ constexpr int kBlk = 3 * kBz + 16;              // one face block: 73 slots
 #define VCT_K4_F43 1
 #endif
 constexpr int kBlk3 = 2 * kBz + 16;
+// brick origin counts from the SCC of the masking s_and_b64 (1) or s_cmp / s_cselect (0)
+#ifndef VCT_K4_ORIGIN_SCC
+#define VCT_K4_ORIGIN_SCC 1
+#endif
+// a step that restages one level runs a staging copy per level (1) instead of selecting
+// the level, mode and origin between the two (0)
+#ifndef VCT_K4_STSPLIT
+#define VCT_K4_STSPLIT 1
+#endif
 // float4 slots per cache entry: up to 4 face blocks (3 without the four-face union)
 // The two cache entries live in LDS regions 0 and 1 (entry a in region `flip`): 9344 B
 // per wave with the union (4 waves/SIMD fit the 160 KB), 7008 B without (5 waves/SIMD).
@@ -604,8 +632,17 @@ __device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl,
     const int b = __builtin_amdgcn_readlane(v, fl);
     const int sg = 1 - 2 * negb;                       // +1 / -1
     const int sv = __mul24(v, sg), sb = b * sg;        // mirrored toward -axis
+#if VCT_K4_ORIGIN_SCC
+    // cnt = (m1 & am != 0) + (m2 & am != 0) from the SCC that s_and_b64 sets (4 scalar
+    // instructions instead of two masks, two compare / select pairs and an add)
+    unsigned long long m2 = wballot(sv < sb - 1), m1 = wballot(sv < sb);   // m2 within m1
+    int cnt;
+    asm("s_and_b64 %1, %1, %3\n\ts_cselect_b32 %0, 1, 0\n\ts_and_b64 %2, %2, %3\n\ts_addc_u32 %0, %0, 0"
+        : "=&s"(cnt), "+s"(m1), "+s"(m2) : "s"(am) : "scc");
+#else
     const unsigned long long m2 = wballot(sv < sb - 1) & am, m1 = wballot(sv < sb) & am;   // m2 within m1
     const int cnt = s_nonzero(m1) + s_nonzero(m2);
+#endif
     return b - sg * cnt - back * negb;      // back = brick depth - 2
 }
 
@@ -632,7 +669,7 @@ __device__ __forceinline__ int lane_id_opaque() {
 struct Tex4 { float4 a, b, c, d; };
 
 // this lane's staging texel: iso -> a; comb / faces -> faces f0..f3 of the union in a..d
-template <bool O32>
+template <bool O32, int AM = -1>   // AM: see step_bricks
 __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEntry& be, int mode,
                                            const ConeCtl& cc) {
     const int nl = k.n >> l;
@@ -659,7 +696,7 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
         t.a = lv.fetch(((uint32_t)cc.f0 << sh) + gi, inb);
         t.b = lv.fetch(((uint32_t)cc.f1 << sh) + gi, inb);
         t.c = lv.fetch(((uint32_t)cc.f2 << sh) + gi, inb);
-        if (cc.nfaces > 3) t.d = lv.fetch(((uint32_t)cc.f3 << sh) + gi, inb);
+        if (AM != kComb && cc.nfaces > 3) t.d = lv.fetch(((uint32_t)cc.f3 << sh) + gi, inb);
     }
     return t;
 }
@@ -669,6 +706,7 @@ __device__ __forceinline__ uint32_t bits4(float4 v) {
 }
 
 // stores this lane's staging texel(s); returns true when every value it stored is +0
+template <int AM = -1>
 __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const Tex4& t, float4* __restrict__ lds) {
     const int lane = lane_id_opaque();
     float4* p = lds + ((lane & 15) + kBz * (lane >> 4));
@@ -676,7 +714,7 @@ __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const T
     if (mode == kIso) {
         p[0] = t.a;
         nz = bits4(t.a);
-    } else if (mode == kComb) {     // f0, f1, f2 = the x, y, z faces
+    } else if (AM == kComb || mode == kComb) {     // f0, f1, f2 = the x, y, z faces
         const float4 v = combine3(cc.uwx, cc.uwy, cc.uwz, t.a, t.b, t.c);
         p[0] = v;
         nz = bits4(v);
@@ -777,7 +815,9 @@ struct LaneDir {
 // One step's blended sample (1 - fr) D_{l0} + fr D_{l0+1} for a wave-uniform l0.
 // Each level is served from the cache, restaged (both levels' loads in one
 // batch) or, when the wave's footprint does not fit, gathered per lane.
-template <bool O32, bool UNION, int KL>
+// AM: the cone's anisotropic staging mode when march_brick specialised the march on it
+// (kComb for dir_uniform cones, kFaces otherwise; -1 = read cc.dir_uniform per step)
+template <bool O32, bool UNION, int KL, int AM = -1>
 __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx, float qy, float qz,
                                               unsigned long long amA, unsigned long long amB, float fr, const ConeCtl& cc, const LaneDir& ld,
                                               float4* __restrict__ lds, BrickCache& bc, PhaseClock& pc) {
@@ -787,12 +827,13 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const bool activeB = __builtin_amdgcn_inverse_ballot_w64(amB);
     const bool needB = amB != 0ull;
     const int l1 = l0 + 1;                     // needB implies l0 < L
-    const int aniso_mode = cc.dir_uniform ? kComb : kFaces;
+    const int aniso_mode = AM >= 0 ? AM : (cc.dir_uniform ? kComb : kFaces);
     const int modeA = (l0 == 0 || !k.aniso) ? kIso : aniso_mode;
     const int modeB = k.aniso ? aniso_mode : kIso;
-    const bool faces_ok = UNION || VCT_K4_F43 ? cc.nfaces <= 4 : cc.nfaces == 3;
+    const bool faces_ok = AM == kComb || (UNION || VCT_K4_F43 ? cc.nfaces <= 4 : cc.nfaces == 3);
     // faces-mode levels of a four-face cone in the occupancy form: 4 x 4 x 3 bricks
-    const int z3A = modeA == kFaces ? cc.z3 : 0, z3B = modeB == kFaces ? cc.z3 : 0;
+    // (a dir_uniform cone has three faces: never z3)
+    const int z3A = AM != kComb && modeA == kFaces ? cc.z3 : 0, z3B = AM != kComb && modeB == kFaces ? cc.z3 : 0;
     if (bc.a.lvl != l0 && bc.b.lvl == l0) {       // the level advanced by one: b becomes a
         // a cone's level never decreases, so the old a (level l0 - 1) is dead: b moves into
         // a's place, b is emptied and the LDS regions trade roles (no three-way swap)
@@ -842,16 +883,22 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // zero (fmaf(w, +0, +0) = +0 through the whole trilinear chain), so hits on it skip
     // the LDS reads and the FMAs
     if (stA && stB) {
-        const Tex4 tA = stage_load<O32>(k, l0, bA, modeA, cc);
-        const Tex4 tB = stage_load<O32>(k, l1, bB, modeB, cc);
-        const bool zA = stage_store(modeA, cc, tA, ldsA);
-        const bool zB = stage_store(modeB, cc, tB, ldsB);
+        const Tex4 tA = stage_load<O32, AM>(k, l0, bA, modeA, cc);
+        const Tex4 tB = stage_load<O32, AM>(k, l1, bB, modeB, cc);
+        const bool zA = stage_store<AM>(modeA, cc, tA, ldsA);
+        const bool zB = stage_store<AM>(modeB, cc, tB, ldsB);
         bA.zero = bc.a.zero = wall(zA);
         bB.zero = bc.b.zero = wall(zB);
         wave_lds_sync();
+    } else if (VCT_K4_STSPLIT && stA) {
+        bA.zero = bc.a.zero = wall(stage_store<AM>(modeA, cc, stage_load<O32, AM>(k, l0, bA, modeA, cc), ldsA));
+        wave_lds_sync();
+    } else if (VCT_K4_STSPLIT && stB) {
+        bB.zero = bc.b.zero = wall(stage_store<AM>(modeB, cc, stage_load<O32, AM>(k, l1, bB, modeB, cc), ldsB));
+        wave_lds_sync();
     } else if (stA || stB) {
         const int mode = stA ? modeA : modeB;
-        const bool z = wall(stage_store(mode, cc, stage_load<O32>(k, stA ? l0 : l1, stA ? bA : bB, mode, cc),
+        const bool z = wall(stage_store<AM>(mode, cc, stage_load<O32, AM>(k, stA ? l0 : l1, stA ? bA : bB, mode, cc),
                                         stA ? ldsA : ldsB));
         if (stA) bA.zero = bc.a.zero = z;
         else bB.zero = bc.b.zero = z;
@@ -870,10 +917,10 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         // corner-0 texels instead of its own (staged, finite), and its march adds nothing
         // (march_brick scales the sample by 0)
         if (readA)
-            sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA) : 0, modeA != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr), ld.bz(cc.bstr),
+            sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA) : 0, AM == kComb || modeA != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr), ld.bz(cc.bstr),
                                   ld.wx(), ld.wy(), ld.wz(), ldsA);
         if (readB)
-            sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB) : 0, modeB != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr),
+            sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB) : 0, AM == kComb || modeB != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr),
                                   ld.bz(cc.bstr), ld.wx(), ld.wy(), ld.wz(), ldsB);
         wave_lds_sync();
     }
@@ -1046,6 +1093,12 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     BrickCache bc;
     bc.a = bc.b = BrickEntry{-1, 0, 0, 0, 0};
     bc.flip = 0;
+    // The march is compiled once per anisotropic staging mode (VCT_K4_AMSPEC): a
+    // dir_uniform cone (flat surfaces) stages combined faces at every anisotropic level,
+    // any other cone stages face blocks, so the per-step mode selects, the four-face /
+    // z3 tests and the faces-mode sampling fold away in the combined-face copy.
+    auto march_loop = [&](auto am_tag) __attribute__((always_inline)) {
+    constexpr int AM = decltype(am_tag)::value;
     for (int i = 0;; ++i) {
         asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz), "+v"(ld.blk));   // see LaneDir
         ld.dx = dx; ld.dy = dy; ld.dz = dz;
@@ -1091,7 +1144,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         if (TAB || wall_in(am, l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
             if (VCT_K4_PRIO) __builtin_amdgcn_s_setprio(0);   // default priority for the step head, brick geometry and staging
-            s = step_bricks<O32, UNION, KL>(k, l0f, qx, qy, qz, am, am & two_m, fr, cc, ld, lds, bc, pc);
+            s = step_bricks<O32, UNION, KL, AM>(k, l0f, qx, qy, qz, am, am & two_m, fr, cc, ld, lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
             s = sample_level<O32, false, gather_chunk<UNION>()>(k, l0, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(),
                                                                   ld.wy(), ld.wz());
@@ -1118,6 +1171,15 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         }
         pc.mark(5);
     }
+    };
+#ifndef VCT_K4_AMSPEC
+#define VCT_K4_AMSPEC 2
+#endif
+    // 1: every march; 2: the table marches only
+    constexpr bool kAmSpec = VCT_K4_AMSPEC == 1 || (VCT_K4_AMSPEC == 2 && TAB);
+    if (kAmSpec && cc.dir_uniform) march_loop(std::integral_constant<int, kComb>{});
+    else if (kAmSpec) march_loop(std::integral_constant<int, kFaces>{});
+    else march_loop(std::integral_constant<int, -1>{});
     res = make_float4(cr, cg, cb, a);
     return steps;
 }
@@ -1552,7 +1614,13 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     const Grid& g = c->grid;
     TraceK k;
     k.pyr = g.pyr;
-    for (int i = 0; i <= kMaxLevels; ++i) k.lvl_off[i] = g.lvl_off[i];
+    for (int i = 0; i <= kMaxLevels; ++i) {
+        k.lvl_off[i] = g.lvl_off[i];
+        // level i's bytes (all faces): n_i^3 texels x 16 B, x 6 faces above level 0 when anisotropic
+        const uint64_t ni = i <= (int)g.L ? (uint64_t)(g.n >> i) : 0u;
+        const uint64_t by = ni * ni * ni * 16u * (i > 0 && g.aniso ? 6u : 1u);
+        k.lvl[i] = LevelRange{g.pyr + g.lvl_off[i], by <= 0xffffffffull ? (uint32_t)by : 0u, 0u};   // 2 GiB at 512^3
+    }
     k.n = (int)g.n; k.L = (int)g.L;
     k.lgn = __builtin_ctz(g.n);
     k.g0x = g.g0[0]; k.g0y = g.g0[1]; k.g0z = g.g0[2];
