@@ -127,7 +127,7 @@ __constant__ float c_cones9[9][4] = {VCT_CONES9(VCT_CROW)};
 __constant__ float c_cones16[16][4] = {VCT_CONES16(VCT_CROW)};
 
 // level l's buffer range as the O32 kernels bind it (one 16-B scalar load per level view)
-struct LevelRange {
+struct alignas(16) LevelRange {
     const float4* base;          // pyr + lvl_off[l]
     uint32_t bytes;              // the level's size (every face; num_records is unsigned), 0 above 32 bits
     uint32_t pad;
@@ -538,6 +538,10 @@ constexpr int kBlk = 3 * kBz + 16;              // one face block: 73 slots
 #define VCT_K4_F43 1
 #endif
 constexpr int kBlk3 = 2 * kBz + 16;
+// the two-level test of table rows on the scalar unit from fr's bits (1)
+#ifndef VCT_K4_TWOS
+#define VCT_K4_TWOS 1
+#endif
 // brick origin counts from the SCC of the masking s_and_b64 (1) or s_cmp / s_cselect (0)
 #ifndef VCT_K4_ORIGIN_SCC
 #define VCT_K4_ORIGIN_SCC 1
@@ -1103,11 +1107,12 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz), "+v"(ld.blk));   // see LaneDir
         ld.dx = dx; ld.dy = dy; ld.dz = dz;
         float D, fr;
-        int l0;
+        int l0, frb = 0;
         if constexpr (TAB) {                    // wave-uniform row i
             t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tab.t), i));
             D = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tab.D), i));
-            fr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tab.fr), i));
+            frb = __builtin_amdgcn_readlane(__float_as_int(tab.fr), i);
+            fr = __int_as_float(frb);
             l0 = __builtin_amdgcn_readlane(tab.l0, i);
         }
         const float qx = ox + dx * t, qy = oy + dy * t, qz = oz + dz * t;
@@ -1136,7 +1141,14 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         // both levels sampled: fr > 0 (fr >= +0 here, so a nonzero bit pattern) and l0 < L;
         // for table rows both are wave-uniform: a scalar test, no VALU compare and ballot
         unsigned long long two_m;
+#if VCT_K4_TWOS
+        // on the scalar unit from fr's bits (LLVM otherwise turns the bit test into a VALU class test)
+        if constexpr (TAB)
+            asm("s_cmp_lg_u32 %1, 0\n\ts_cselect_b64 %0, -1, 0\n\ts_cmp_lt_i32 %2, %3\n\ts_cselect_b64 %0, %0, 0"
+                : "=&s"(two_m) : "s"(frb), "s"(l0), "s"(k.L) : "scc");
+#else
         if constexpr (TAB) two_m = ((__float_as_uint(fr) != 0u) & (l0 < k.L)) ? ~0ull : 0ull;
+#endif
         else two_m = wballot(fr > 0.0f) & wballot(l0 < k.L);
         const bool two = __builtin_amdgcn_inverse_ballot_w64(two_m);
         const int l0f = TAB ? l0 : __builtin_amdgcn_readlane(l0, __builtin_ctzll(am));
