@@ -23,7 +23,7 @@ forces it); every timed step still traces, exchanges and un-permutes one
 whole frame, and the pipeline is drained inside the timed region.  The
 roofline's K4 launch duration (`k4_kernel_ms_avg`) is timed after the loop
 with K frames back to back on one stream (the kernel alone; rocprofv3 agrees
-with it on a `--overlap off` run, profiles/r03_r3m_*); `k4_kernel_ms_avg_overlapped`
+with it on a `--overlap off` run, profiles/r03_r3n_ovoff_*); `k4_kernel_ms_avg_overlapped`
 is the launches' start-to-end average inside the pipelined loop, where two
 traces share the chip, and `roofline.pipelined` the same per-launch work over
 the timed loop's time per frame.  The level-0 grid is injected
