@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--scene", default="atrium")
     ap.add_argument("--clk", action="store_true", help="phase clocks (make clk) instead of path counters")
     ap.add_argument("--variants", default="0")
+    ap.add_argument("--nd", type=int, default=9, help="diffuse cones (0 = the specular cone alone)")
+    ap.add_argument("--spec", type=int, default=1, help="specular cone on/off")
     a = ap.parse_args()
     import torch
     from vct import Context, _lib, scenes
@@ -37,7 +39,7 @@ def main():
     lib.vct_debug_counters.argtypes = [C.c_void_p, C.c_int]
     ctr = (C.c_ulonglong * 48)()
     g0, E = scenes.grid_for_unit_box(a.n)
-    ctx = Context(a.n, g0, E)
+    ctx = Context(a.n, g0, E, n_diffuse=a.nd, specular=bool(a.spec))
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     s = scenes.SCENES[a.scene]()
     ctx.voxelize(*s.arrays())
