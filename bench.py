@@ -66,6 +66,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import datetime
 import hashlib
 import json
 import math
@@ -197,16 +198,21 @@ def load_profile(path, key):
     return rec, None
 
 
-def roofline(rec, reason, k4_ms, texels, valid_px, profile_path, key):
-    gather = texels * BYTES_PER_TEXEL + valid_px * BYTES_PER_VALID_PX
-    t = k4_ms * 1e-3
+def roofline(rec, reason, k4_ms, texels, valid_px, profile_path, key, steps=None):
+    """k4_ms None: the record's own rocprofv3 kernel duration is the live time (a line that
+    times whole frames only, e.g. `stress`, whose frames include the reorder sort)."""
+    if k4_ms is None and rec is not None:
+        k4_ms = rec.get("duration_ms")
+    gather = texels * BYTES_PER_TEXEL + valid_px * BYTES_PER_VALID_PX if texels is not None else None
     out = {"bound": "issue (VALU)", "achieved": None, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s", "frac": None,
-           "traffic": None, "gather_bytes": gather, "gather_GBs": round(gather / t / 1e9, 1),
-           "texel_fetches_per_launch": texels,
+           "traffic": None, "gather_bytes": gather,
+           "gather_GBs": round(gather / (k4_ms * 1e-3) / 1e9, 1) if gather is not None and k4_ms else None,
+           "texel_fetches_per_launch": texels, "k4_ms": round(k4_ms, 4) if k4_ms else None,
            "peak_basis": "1024 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
-    if rec is None:
-        out["note"] = reason
+    if rec is None or not k4_ms:
+        out["note"] = reason or "no kernel time"
         return out
+    t = k4_ms * 1e-3
     valu, salu = rec["SQ_INSTS_VALU"], rec["SQ_INSTS_SALU"]
     hbm = rec["hbm_bytes_per_launch"]
     v_ach = valu / t / 1e9
@@ -221,7 +227,16 @@ def roofline(rec, reason, k4_ms, texels, valid_px, profile_path, key):
                 "frac": round(h_ach / HBM_PEAK_GBS, 4)},
         "profile": f"{os.path.relpath(profile_path, REPO)}#{key}",
         "profile_kernel_ms": rec.get("duration_ms"),
+        "profile_tag": rec.get("tag"),
     })
+    if steps:
+        # wave instructions per cone step (a wave-step advances ~62 lanes' cone steps)
+        out["valu_per_cone_step"] = round(valu / steps, 3)
+        out["salu_per_cone_step"] = round(salu / steps, 3)
+    if rec.get("SQ_WAVE_CYCLES"):
+        # fraction of wave cycles in which the wave issued (the rest: waits and issue stalls)
+        out["issue_active"] = round(rec["SQ_ACTIVE_INST_ANY"] / rec["SQ_WAVE_CYCLES"], 4)
+        out["wait_any"] = round(rec["SQ_WAIT_ANY"] / rec["SQ_WAVE_CYCLES"], 4)
     out["valu"] = {"achieved": out["achieved"], "peak": VALU_PEAK_G, "unit": out["unit"], "frac": out["frac"]}
     # name the resource that binds: the most loaded of VALU issue, scalar issue and HBM
     if out["salu"]["frac"] > max(out["frac"], out["hbm"]["frac"]):
@@ -609,7 +624,7 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
         "value": frame_steps * args.steps / elapsed / 1e6, "ms_per_step": ms_per_step, "frame_cone_steps": frame_steps,
         "valid_px": frame_valid, "k4_kernel_ms_avg": k4_avg_ms, "k4_kernel_ms_median": k4_med_ms,
         "k4_kernel_ms_avg_overlapped": sum(k4_ov_ms) / len(k4_ov_ms), "overlap": tracer.overlap,
-        "local_texels": local_texels, "local_valid": local_valid,
+        "local_texels": local_texels, "local_valid": local_valid, "local_steps": local_steps,
         "frame_relight_ms": round(min(k2_ms + bcast_ms, k2_rep_ms) + k3_ms + ms_per_step, 3),
         "frame_relight_bcast_ms": round(k2_ms + bcast_ms + k3_ms + ms_per_step, 3),
         "frame_relight_replicated_ms": round(k2_rep_ms + k3_ms + ms_per_step, 3),
@@ -723,11 +738,16 @@ def measure_config(args, torch, dist, rank, world, dev, stream, cfg):
     ctx = Context(a.n, g0, E, aniso=True, n_diffuse=a.n_diffuse, specular=not args.no_spec, device=dev.index)
     ctx.set_stream(stream.cuda_stream)
     m = measure_scene(a, torch, dist, ctx, cfg["scene"], rank, world, dev, stream)
+    key = profile_key(a.n, a.width, a.height, cfg["scene"], "scene", a.n_diffuse, not args.no_spec, args.variant, world)
+    roof = roofline(*load_profile(args.profile_json, key), m["k4_kernel_ms_avg"], m["local_texels"], m["local_valid"],
+                    args.profile_json, key, steps=m["local_steps"])
     out = {"workload": f"{cfg['scene']}{STAND_IN.get(cfg['scene'], '')}, {a.n}^3 aniso RGBA32F, "
                        f"{a.width}x{a.height}, {a.n_diffuse}+{0 if args.no_spec else 1} cones",
            "value": round(m["value"], 2), "unit": "Mcone-steps/s", "ms_per_step": round(m["ms_per_step"], 4),
            "frame_cone_steps": m["frame_cone_steps"], "k4_kernel_ms_avg_rank0": round(m["k4_kernel_ms_avg"], 4),
-           "k4_form_rank0": form_name(m["k4_form"]), "overlap_tune_rank0": m["overlap_tune"]}
+           "k4_form_rank0": form_name(m["k4_form"]), "overlap_tune_rank0": m["overlap_tune"],
+           "value_single_launch": round(m["frame_cone_steps"] / m["k4_kernel_ms_avg"] / 1e3, 2) if world == 1 else None,
+           "roofline_rank0": roof}
     for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
                "replicated_k2_equals_bcast", "trace_ms_max_rank", "gather_ms", "allgather_ms"):
         if k_ in m:
@@ -757,6 +777,8 @@ def capi_leg(args, torch, dist, ctx, rank, world, dev, stream, gb, eye):
     cid = share_comm_id(dist, rank)
     ctx.comm_set_timeout(120000)
     ctx.comm_init(cid, world, rank)
+    c_rank, c_n = ctx.comm_rank()           # what the RCCL communicator itself holds
+    ok_ranks = max_over_ranks(torch, dist, dev, [0.0 if (c_rank, c_n) == (rank, world) else 1.0], world)[0] == 0.0
     n = ctx.n
     before = torch.empty((n ** 3 * 4,), dtype=torch.float32, device=dev)
     after = torch.empty_like(before)
@@ -772,7 +794,7 @@ def capi_leg(args, torch, dist, ctx, rank, world, dev, stream, gb, eye):
     bcast_ok = bool(torch.equal(before, after))
     del before, after
     ctx.build_mips()
-    out = {"bcast_equal": bcast_ok}
+    out = {"bcast_equal": bcast_ok, "vct_comm_nranks": c_n, "vct_comm_ranks_match": ok_ranks}
     d, sp = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
     for root, name in ((0, "present"), (VCT_ALL_RANKS, "allgather")):
         d.fill_(-1.0)
@@ -838,7 +860,13 @@ def stress_rand(args, torch, ctx, dev, stream):
     (a0, a1), (b0, b1), (c0, c1) = outs.values()
     t0, t1, t2 = ms.values()
     loop = frame_loop(torch, ctx, gb, w, h, eye, stream, args.frame_loop, variant=auto) if args.frame_loop else None
+    key = profile_key(args.n, w, h, args.scene, "rand", args.n_diffuse, not args.no_spec, args.variant, 1)
+    rec, reason = load_profile(args.profile_json, key)
+    # whole frames are timed here (the reorder keys and sort included), so the roofline's
+    # live time is the record's own rocprofv3 K4 duration
+    roof = roofline(rec, reason, None, None, w * h, args.profile_json, key, steps=steps)
     return {"gbuffer": "G_rand (seed 42), same grid", "frame_cone_steps": steps, "frames": reps, "_loop": loop,
+            "roofline": roof,
             "screen_order_ms": round(t0, 4), "reordered_ms": round(t1, 4), "default_ms": round(t2, 4),
             "screen_order_Mcone_steps_s": round(steps / t0 / 1e3, 2),
             "reordered_Mcone_steps_s": round(steps / t1 / 1e3, 2),
@@ -864,10 +892,14 @@ def run(args, world):
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     if world > 1:
+        # a collective that cannot complete (a rank died or hangs) ends every rank with an
+        # error after 120 s -- inside the driver's 600 s bench limit -- instead of torch's
+        # default 10-minute timeout killing the run without a line
+        pg_timeout = datetime.timedelta(seconds=float(os.environ.get("VCT_PG_TIMEOUT_S", "120")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=pg_timeout)
 
     from vct import Context, scenes
 
@@ -883,7 +915,8 @@ def run(args, world):
     progress(rank, f"metric done: {m['value']:.0f} Mcone-steps/s")
     key = profile_key(n, w, h, args.scene, args.gbuffer, args.n_diffuse, spec, args.variant, world)
     rec, reason = load_profile(args.profile_json, key)
-    roof = roofline(rec, reason, m["k4_kernel_ms_avg"], m["local_texels"], m["local_valid"], args.profile_json, key)
+    roof = roofline(rec, reason, m["k4_kernel_ms_avg"], m["local_texels"], m["local_valid"], args.profile_json, key,
+                    steps=m["local_steps"])
     if roof.get("frac") is not None and m["ms_per_step"] > 0:
         # the same per-launch work over the pipelined frame time: with frame overlap a launch's
         # own start-to-end time includes the other frame's share of the chip, so the rate the
@@ -918,6 +951,19 @@ def run(args, world):
         }
         for k_ in ("frame_cone_steps", "valid_px"):
             result[k_] = m[k_]
+        # latency beside throughput: `value` pipelines consecutive frames (frame f+1's trace
+        # fills the tail of frame f's launch), so a launch inside the loop runs longer from
+        # start to end than alone; a renderer that presents each frame before tracing the
+        # next gets `value_single_launch` (frame steps / the launch alone)
+        if world == 1:
+            result["value_single_launch"] = round(m["frame_cone_steps"] / m["k4_kernel_ms_avg"] / 1e3, 2)
+        else:
+            tr, ex = m.get("trace_ms_max_rank"), m.get("gather_ms" if args.exchange == "present" else "allgather_ms")
+            result["value_unpipelined"] = round(m["frame_cone_steps"] / (tr + ex) / 1e3, 2) if tr and ex else None
+        result["latency"] = {"k4_launch_ms_alone": round(m["k4_kernel_ms_avg"], 4),
+                             "k4_launch_ms_in_pipelined_loop": round(m["k4_kernel_ms_avg_overlapped"], 4),
+                             "frame_ms_pipelined": round(m["ms_per_step"], 4),
+                             "frames_in_flight": 2 if m["overlap"] or world > 1 else 1}
         result["k4_kernel_ms_avg"] = round(m["k4_kernel_ms_avg"], 4)
         result["k4_kernel_ms_median"] = round(m["k4_kernel_ms_median"], 4)
         result["k4_kernel_ms_avg_overlapped"] = round(m["k4_kernel_ms_avg_overlapped"], 4)
@@ -960,6 +1006,12 @@ def run(args, world):
                     "present_frame_ms": None, "allgather_frame_ms": None, "bcast_ms": None}
         if rank == 0:
             result["capi"] = capi
+            # what the collectives ran over: torch's process group and the C-ABI's own
+            # RCCL communicator (vct_comm_rank after vct_comm_init)
+            result["rccl"] = {"backend": dist.get_backend(), "pg_world": dist.get_world_size(),
+                              "pg_timeout_s": float(os.environ.get("VCT_PG_TIMEOUT_S", "120")),
+                              "vct_comm_nranks": (capi or {}).get("vct_comm_nranks"),
+                              "vct_comm_ranks_match": (capi or {}).get("vct_comm_ranks_match")}
     del m
     torch.cuda.empty_cache()
     st = (args.stress or "").strip()
@@ -981,7 +1033,13 @@ def run(args, world):
                 "ms_per_step": round(s2["ms_per_step"], 4), "k4_kernel_ms_avg": round(s2["k4_kernel_ms_avg"], 4),
                 "frame_cone_steps": s2["frame_cone_steps"], "valid_px": s2["valid_px"],
                 "k1_voxelize_ms": s2["k1_voxelize_ms"], "k4_form": form_name(s2["k4_form"]),
+                "value_single_launch": round(s2["frame_cone_steps"] / s2["k4_kernel_ms_avg"] / 1e3, 2)
+                if world == 1 else None,
             }
+            key2 = profile_key(n, w, h, sec, args.gbuffer, args.n_diffuse, spec, args.variant, world)
+            result["secondary"]["roofline"] = roofline(*load_profile(args.profile_json, key2), s2["k4_kernel_ms_avg"],
+                                                       s2["local_texels"], s2["local_valid"], args.profile_json, key2,
+                                                       steps=s2["local_steps"])
             if "trace_ms_max_rank" in s2:
                 result["secondary"]["trace_ms_max_rank"] = s2["trace_ms_max_rank"]
         del s2

@@ -23,7 +23,12 @@
  *    the ctx stream between vct_trace_device calls so that consecutive frames
  *    run concurrently on different streams (vct.multi.FrameTracer does, for
  *    1.14x at 1080p): the trace's scratch belongs to the stream (4 streams;
- *    a fifth one frees every set after a device synchronize).  Grid
+ *    a fifth one frees every set after a device synchronize).  The frame
+ *    exchanges of a multi-device context (vct_trace_device on a
+ *    vct_create_multi ctx) and of vct_comm_trace_frame share one gather
+ *    buffer: each such call first waits (on the device, not the host) for the
+ *    previous one, whatever stream either ran on, so they stay correct but do
+ *    not overlap; vct_comm_synchronize covers the last exchange on any stream.  Grid
  *    updates (voxelize / inject / build_mips / uploads) must be ordered
  *    against traces on other streams by the host (events).
  *  - Data layouts: grids cross the ABI linear-Z RGBA32F, index x + n*(y + n*z)
@@ -270,8 +275,9 @@ vct_status vct_comm_destroy(vct_ctx* ctx);
  * (vct_comm_init again to continue), so a dead or absent peer ends the frame loop
  * instead of hanging it. */
 vct_status vct_comm_set_timeout(vct_ctx* ctx, uint32_t timeout_ms);
-/* Waits until the ctx stream's queued work -- collectives included -- has finished,
- * polling the stream and the communicator with the deadline above. */
+/* Waits until the ctx stream's queued work -- collectives included -- and the last
+ * frame exchange (vct_comm_trace_frame on any stream) have finished, polling the
+ * stream, that exchange's end event and the communicator with the deadline above. */
 vct_status vct_comm_synchronize(vct_ctx* ctx);
 /* Where a rank's tiles sit in the exchange buffer of vct_comm_trace_frame (and of the
  * vct.multi driver), in 64x64 tiles: packed for root >= 0 (rank r's [diffuse][spec]

@@ -148,6 +148,17 @@ def png_cases():
     img = rng.integers(0, 256, (11, 10, 4))
     for ft in range(5):
         cases[f"rgba_filter{ft}"] = write_png(img, 6, 8, filters=[ft], extra=False)
+    # headers that declare a huge image over a few bytes of data: stb refuses the first
+    # two as too large (2^30 / w / channels < h; a palette image counts 4 channels), the
+    # third is at the limit and fails for want of pixels -- none may size a buffer from
+    # the header alone (host/png.cpp)
+    for name, (w, h, color, plte) in {"huge_rgba": (1 << 15, 1 << 15, 6, None),
+                                      "huge_pal": (1 << 14, 1 << 15, 3, [[1, 2, 3]]),
+                                      "limit_gray": (1 << 15, 1 << 15, 0, None)}.items():
+        out = b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, color, 0, 0, 0))
+        if plte is not None:
+            out += _chunk(b"PLTE", bytes(np.asarray(plte, np.uint8).reshape(-1)))
+        cases[name] = out + _chunk(b"IDAT", zlib.compress(bytes(64), 9)) + _chunk(b"IEND", b"")
     return cases
 
 

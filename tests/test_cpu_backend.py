@@ -276,6 +276,11 @@ def test_device_pointer_checks(cpu_lib):
                          tile_compact=True)
     with pytest.raises(VctError, match="EINVAL.*64-bit"):
         ctx.voxelize_device(F(14 * 3, shape=(3, 14)), F(3, dtype="torch.int64"))
+    # the C-ABI bounds kd4 and the material map by one n_mat: a map longer than kd4 is
+    # refused (K1 would read kd4 past its end on the device), as on the host path
+    with pytest.raises(VctError, match="EINVAL.*material_map has 3 entries for 2 materials"):
+        ctx.voxelize_device(F(14 * 3, shape=(3, 14)), F(3, dtype="torch.int32"), F(1, dtype="torch.int32"),
+                            F(8, shape=(2, 4)), material_map=F(3, dtype="torch.int32"))
 
 
 def test_comm_one_rank(cpu_lib):

@@ -206,8 +206,7 @@ def test_occupancy_form_curved_bitexact(gpu_ready, oracle_mod, kind):
 
 @pytest.mark.parametrize("kind", ["scene", "rand", "mirror", "jitter"])
 def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
-    """The K4 variants (0 = LDS bricks, 1 = per-lane gathers, 2 = bricks without
-    the four-face union, 3 = row-major lanes; bit 0x100 = no specular step tables,
+    """The K4 variants (0 = LDS bricks, 1 = per-lane gathers; bit 0x100 = no specular step tables,
     0x200 = all cones in one workgroup, 0x400 / 0x800 = cones split over three /
     two workgroups) equal the oracle bit for bit.  Without per-pixel step counts
     the default splits the cones over workgroups (three parts for small launches,
@@ -222,9 +221,9 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     gb = [torch.from_numpy(a).to(dev) for a in (pos, nrm, alb)]
     ref = O.trace(n, g0, E, ctx.download_level(0), gpu_pyramid_flat(ctx), pos, nrm, alb, cam.position)
-    # 0x8000: rays reordered by the Morton code of their origin voxel (alone, with gathers, without the union)
+    # 0x8000: rays reordered by the Morton code of their origin voxel (alone, with gathers)
     # 0x1000000 / 0x2000000: the union / occupancy form of the default variant
-    for variant in (0, 1, 2, 3, 0x8000, 0x8001, 0x8002, 0x1000000, 0x2000000, 0x2008000, 0x4000000, 0x5000000):
+    for variant in (0, 1, 0x8000, 0x8001, 0x1000000, 0x2000000, 0x2008000, 0x4000000, 0x5000000):
         d = torch.empty((h, w, 4), device=dev)
         sp = torch.empty((h, w, 4), device=dev)
         st = torch.zeros((h, w), dtype=torch.int32, device=dev)
@@ -240,7 +239,7 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
     # bits 20-23: diffuse parts of the split (3, 4 -> 3 parts of 3 cones, 5, 9 -> one cone each)
     for variant in (0, 1, 0x100, 0x200, 0x400, 0x800, 0x400, 0x300400, 0x400400, 0x500400, 0x900400, 0x900400,
                     0x500400, 0, 0x8000, 0x8400, 0x8800, 0x8200, 0x8000, 0x1000000, 0x2000000, 0x2000400,
-                    0x2000800, 0x2001000, 0x2008000, 0x4000000, 0x6000000, 0):
+                    0x2000800, 0x2008000, 0x4000000, 0x6000000, 0):
         d = torch.full((h, w, 4), -1.0, device=dev)
         sp = torch.full((h, w, 4), -1.0, device=dev)
         cnt = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -258,6 +257,11 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         torch.cuda.synchronize()
         assert np.array_equal(d.cpu().numpy(), ref["diffuse"]), f"variant {variant:#x} diffuse (no counters)"
         assert np.array_equal(sp.cpu().numpy(), ref["spec"]), f"variant {variant:#x} spec (no counters)"
+    # variants retired in round 4 (vct_variants.h) are refused, not silently remapped
+    from vct import VctError
+    for variant in (2, 3, 0x1000, 0x2000, 0x8002):
+        with pytest.raises(VctError):
+            ctx.trace_device(*gb, w, h, cam.position, d, sp, variant=variant)
     ctx.close()
 
 
@@ -372,6 +376,23 @@ def test_comm_one_rank_rccl(gpu_ready):
         ctx.comm_trace_frame(pos, nrm, alb, w, h, cam.position, d, sp, root=root)
         torch.cuda.synchronize()
         assert torch.equal(d, full_d) and torch.equal(sp, full_s), root
+    # frames on alternating streams share the gather buffer (ordered on the device by
+    # xchg_enter); comm_synchronize waits for the last exchange of either stream
+    eyes = [(0.0, 0.0, 3.0), (0.2, 0.1, 2.6), (-0.3, 0.2, 2.8)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    outs = []
+    for f, e in enumerate(eyes):
+        ctx.set_stream(streams[f % 2].cuda_stream)
+        d, sp = torch.empty_like(full_d), torch.empty_like(full_s)
+        ctx.comm_trace_frame(pos, nrm, alb, w, h, e, d, sp, root=VCT_ALL_RANKS if f % 2 else 0)
+        outs.append((d, sp))
+    ctx.comm_synchronize()
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    for e, (d, sp) in zip(eyes, outs):
+        ctx.trace_device(pos, nrm, alb, w, h, e, full_d, full_s)
+        torch.cuda.synchronize()
+        assert torch.equal(d, full_d) and torch.equal(sp, full_s), e
     ctx.comm_destroy()
     ctx.close()
 
@@ -913,6 +934,28 @@ def test_multi_device_context(gpu_ready, devices):
         d = torch.empty((h, w, 4), device=dev)
         with pytest.raises(VctError):
             ctx.trace_device(*gb, w, h, cam.position, d, d.clone(), tile_rank=0, tile_world=2)
+    # frames queued on alternating streams without a host wait share the gather buffer:
+    # each exchange waits on the device for the previous one (xchg_enter), so every frame
+    # equals the single-device frame of its eye
+    eyes = [(0.0, 0.0, 3.0), (0.2, 0.1, 2.6), (-0.3, 0.2, 2.8), (0.1, -0.2, 3.2)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    got = []
+    for f, e in enumerate(eyes):
+        st = streams[f % 2]
+        ctx.set_stream(st.cuda_stream)
+        d, sp = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+        with torch.cuda.stream(st):
+            ctx.trace_device(*gb, w, h, e, d, sp)
+        got.append((d, sp))
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    ref.set_stream(torch.cuda.current_stream().cuda_stream)
+    for e, (d, sp) in zip(eyes, got):
+        rd, rs = torch.empty((h, w, 4), device=dev), torch.empty((h, w, 4), device=dev)
+        ref.trace_device(*gb, w, h, e, rd, rs)
+        torch.cuda.synchronize()
+        assert torch.equal(d, rd) and torch.equal(sp, rs), f"{devices} devices: frame on alternating streams, eye {e}"
     ctx.close()
     ref.close()
 

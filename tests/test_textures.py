@@ -75,13 +75,18 @@ def test_png_decoder_matches_reference_stb(host):
     g = np.load(os.path.join(GOLD, "tex_png_cases.npz"))
     names = list(g["names"])
     assert len(names) > 100
+    refused = 0
     for name in names:
         got, err = decode(host, g["png_" + name].tobytes())
         ref = g["stb_" + name]
-        assert ref.size, name      # every generated case is valid for stb
+        if not ref.size:           # stb refused the file (the huge-header cases): so must we
+            assert got is None, name
+            refused += 1
+            continue
         assert got is not None, (name, err)
         assert got.shape == ref.shape, (name, got.shape, ref.shape)
         assert np.array_equal(got, ref), name
+    assert refused == 3       # huge_rgba, huge_pal (stb: "too large"), limit_gray (not enough pixels)
 
 
 def test_png_decoder_refuses_corrupt_files(host):
@@ -93,6 +98,11 @@ def test_png_decoder_refuses_corrupt_files(host):
     bad_ihdr = bytearray(good)
     bad_ihdr[24] = 3                                                      # bit depth 3
     assert "depth" in decode(host, bytes(bad_ihdr))[1]
+    # a header declaring more than stb's 2^30-byte limit (stb_image.h:4837-4845) is refused
+    # before anything is sized from it; so is one within the limit over too little data
+    assert "too large" in decode(host, g["png_huge_rgba"].tobytes())[1]
+    assert "too large" in decode(host, g["png_huge_pal"].tobytes())[1]
+    assert "not enough pixels" in decode(host, g["png_limit_gray"].tobytes())[1]
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_TEX), reason="the reference's texture files exist only in the build container")

@@ -112,6 +112,19 @@ hipError_t k4_scratch(vct_ctx* c, int i, size_t bytes, void** out, bool* fresh) 
     *out = sc.p;
     return hipSuccess;
 }
+hipError_t xchg_enter(vct_ctx* c) {
+    if (c->xchg_done && c->xchg_stream != c->stream) return hipStreamWaitEvent(c->stream, c->xchg_done, 0);
+    return hipSuccess;
+}
+
+hipError_t xchg_leave(vct_ctx* c) {
+    if (!c->xchg_done) {
+        hipError_t e = hipEventCreateWithFlags(&c->xchg_done, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    c->xchg_stream = c->stream;
+    return hipEventRecord(c->xchg_done, c->stream);
+}
 }  // namespace vct
 
 extern "C" {
@@ -277,6 +290,7 @@ void vct_destroy(vct_ctx* c) {
         for (auto& s : ss.sc)
             if (s.p) (void)hipFree(s.p);
     if (c->ev) (void)hipEventDestroy(c->ev);
+    if (c->xchg_done) (void)hipEventDestroy(c->xchg_done);
     for (auto& en : c->k4tune.e)
         for (auto& f : en.ev)
             for (auto& sl : f)
@@ -546,6 +560,7 @@ static vct_status trace_multi(vct_ctx* c, const vct_trace_args* a) {
     const bool counting = a->cone_steps || a->texel_fetches;
     void* gp = nullptr;
     void* cp = nullptr;
+    VCT_HIP(xchg_enter(c), "stream wait (previous exchange)");
     VCT_HIP(scratch_get(c, 8, world * slice, &gp), "gather buffer");
     if (counting) {
         VCT_HIP(scratch_get(c, 9, world * 16, &cp), "counter buffer");
@@ -593,6 +608,7 @@ static vct_status trace_multi(vct_ctx* c, const vct_trace_args* a) {
                 "fold counters");
     float4* f[2] = {(float4*)a->diffuse4, (float4*)a->spec4};
     VCT_HIP(launch_untile(c, (const float4*)gp, 2, w, h, world, f), "untile");
+    VCT_HIP(xchg_leave(c), "event record (exchange end)");
     return VCT_OK;
 }
 

@@ -54,6 +54,18 @@ vct_status nccl_fail(vct_ctx* c, ncclResult_t r, const char* where) {
         if (s_ != VCT_OK) return s_;                           \
     } while (0)
 
+// a call between ncclGroupStart and ncclGroupEnd: deferred to the group end (nothing to
+// poll); on an immediate error the group is closed first (RCCL's thread-local group depth
+// would otherwise stay raised for the next vct_comm_init on this thread), then aborted
+#define VCT_NCCL_IN_GROUP(call, where)                                                          \
+    do {                                                                                        \
+        const ncclResult_t r_ = (call);                                                         \
+        if (r_ != ncclSuccess && r_ != ncclInProgress) {                                        \
+            (void)ncclGroupEnd();                                                               \
+            return comm_abort(c, std::string(where) + ": " + ncclGetErrorString(r_));           \
+        }                                                                                       \
+    } while (0)
+
 #define VCT_HIPC(call, where)                                                                          \
     do {                                                                                               \
         hipError_t e_ = (call);                                                                        \
@@ -139,7 +151,10 @@ vct_status vct_comm_synchronize(vct_ctx* c) {
     VCT_HIPC(hipSetDevice(c->device), "hipSetDevice");
     const Clock::time_point end = deadline_of(c);
     for (;;) {
-        const hipError_t q = hipStreamQuery(c->stream);
+        // the current stream, and the last frame exchange on any stream (each exchange is
+        // ordered after the previous one, so its end event covers them all: xchg_enter)
+        hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess && c->xchg_done) q = hipEventQuery(c->xchg_done);
         ncclResult_t a = ncclSuccess;
         if (ncclCommGetAsyncError(comm_of(c), &a) != ncclSuccess || (a != ncclSuccess && a != ncclInProgress))
             return comm_abort(c, std::string("comm_synchronize: ") + ncclGetErrorString(a));
@@ -224,6 +239,7 @@ vct_status vct_comm_trace_frame(vct_ctx* c, const vct_trace_args* a, int32_t roo
     if (vct_comm_frame_layout(a->width, a->height, R, me, root, &L) != VCT_OK) return cfail(c, VCT_EINVAL, "layout");
     VCT_HIPC(hipSetDevice(c->device), "hipSetDevice");
     void* gp = nullptr;
+    VCT_HIPC(xchg_enter(c), "stream wait (previous exchange)");
     VCT_HIPC(scratch_get(c, 8, L.buffer_tiles * tpx * sizeof(float4) + 256, &gp), "comm gather buffer");
     float4* g = (float4*)gp;
     const uint32_t mine = L.tiles;
@@ -244,28 +260,32 @@ vct_status vct_comm_trace_frame(vct_ctx* c, const vct_trace_args* a, int32_t roo
             VCT_NCCL(ncclAllGather(g + L.diffuse_tile * tpx, g, (size_t)L.exchange_tiles * tpx * 4, ncclFloat32,
                                    comm_of(c), c->stream),
                      "ncclAllGather tiles");
-        return vct_untile_planes_device(c, (const float*)g, 2, a->width, a->height, R, frames);
-    }
-    if (R > 1) {
-        VCT_NCCL(ncclGroupStart(), "ncclGroupStart");
-        if ((int)me == root) {
-            for (uint32_t r = 0; r < R; ++r) {
-                vct_comm_layout Lr;
-                (void)vct_comm_frame_layout(a->width, a->height, R, r, root, &Lr);
-                if (r == me || Lr.tiles == 0) continue;
-                VCT_NCCL(ncclRecv(g + Lr.diffuse_tile * tpx, (size_t)Lr.exchange_tiles * tpx * 4, ncclFloat32, (int)r,
-                                  comm_of(c), c->stream),
-                         "ncclRecv tiles");
+        st = vct_untile_planes_device(c, (const float*)g, 2, a->width, a->height, R, frames);
+    } else {
+        if (R > 1) {
+            VCT_NCCL(ncclGroupStart(), "ncclGroupStart");
+            if ((int)me == root) {
+                for (uint32_t r = 0; r < R; ++r) {
+                    vct_comm_layout Lr;
+                    (void)vct_comm_frame_layout(a->width, a->height, R, r, root, &Lr);
+                    if (r == me || Lr.tiles == 0) continue;
+                    VCT_NCCL_IN_GROUP(ncclRecv(g + Lr.diffuse_tile * tpx, (size_t)Lr.exchange_tiles * tpx * 4,
+                                               ncclFloat32, (int)r, comm_of(c), c->stream),
+                                      "ncclRecv tiles");
+                }
+            } else if (mine) {
+                VCT_NCCL_IN_GROUP(ncclSend(g + L.diffuse_tile * tpx, (size_t)L.exchange_tiles * tpx * 4, ncclFloat32,
+                                           root, comm_of(c), c->stream),
+                                  "ncclSend tiles");
             }
-        } else if (mine) {
-            VCT_NCCL(ncclSend(g + L.diffuse_tile * tpx, (size_t)L.exchange_tiles * tpx * 4, ncclFloat32, root,
-                              comm_of(c), c->stream),
-                     "ncclSend tiles");
+            VCT_NCCL(ncclGroupEnd(), "ncclGroupEnd");
         }
-        VCT_NCCL(ncclGroupEnd(), "ncclGroupEnd");
+        if ((int)me == root)
+            st = vct_untile_planes_packed_device(c, (const float*)g, 2, a->width, a->height, R, frames);
     }
-    if ((int)me != root) return VCT_OK;
-    return vct_untile_planes_packed_device(c, (const float*)g, 2, a->width, a->height, R, frames);
+    if (st != VCT_OK) return st;
+    VCT_HIPC(xchg_leave(c), "event record (exchange end)");
+    return VCT_OK;
 }
 
 }  // extern "C"

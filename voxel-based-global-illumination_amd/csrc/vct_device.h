@@ -45,58 +45,36 @@ __host__ __device__ __forceinline__ float spec_log2(float x) {
 
 // Texel layout of the radiance pyramid in HBM (SURVEY.md A.1 lets the HIP side
 // keep a brick-linear internal layout; vct_download_level / vct_upload_level0
-// convert to / from linear-Z).  VCT_BRICK2 = 1: every face volume of a level is
-// stored as 2x2x2 bricks of 8 consecutive texels (128 B = one cache line; a
-// trilinear footprint touches 1.5^3 = 3.4 lines on average instead of ~4.5
-// rows of a linear-Z volume), bricks in linear-Z order.  0: linear-Z.
-#ifndef VCT_BRICK2
-#define VCT_BRICK2 1
-#endif
+// convert to / from linear-Z).  Every face volume of a level is stored as 2x2x2
+// bricks of 8 consecutive texels (128 B = one cache line; a trilinear footprint
+// touches 1.5^3 = 3.4 lines on average instead of ~4.5 rows of a linear-Z volume;
+// round 2: G_rand HBM traffic 302 -> 254 GB per frame), bricks in linear-Z order.
 
 // index of texel (x, y, z) inside one face volume of nl^3 texels (nl a power of two)
 __host__ __device__ __forceinline__ uint32_t texel_index(uint32_t x, uint32_t y, uint32_t z, uint32_t nl) {
-#if VCT_BRICK2
     const uint32_t nb = nl > 1 ? nl >> 1 : 1u;
     return ((((z >> 1) * nb + (y >> 1)) * nb + (x >> 1)) << 3) | ((z & 1u) << 2) | ((y & 1u) << 1) | (x & 1u);
-#else
-    return x + nl * (y + nl * z);
-#endif
 }
 
 // texel_index for nl = 2^lg from shifts: the same value for every in-range texel
 // (x >> 1 < nb); out-of-range coordinates give an unspecified index (never read)
 __host__ __device__ __forceinline__ uint32_t texel_index_lg(uint32_t x, uint32_t y, uint32_t z, uint32_t lg) {
-#if VCT_BRICK2
     const uint32_t lnb = lg > 0u ? lg - 1u : 0u;
     return (((x >> 1) | ((y >> 1) << lnb) | ((z >> 1) << (2u * lnb))) << 3) | ((z & 1u) << 2) | ((y & 1u) << 1) |
            (x & 1u);
-#else
-    return x + ((y + (z << lg)) << lg);
-#endif
 }
 
 // inverse of texel_index: (x, y, z) of index v in a face volume of nl^3 texels
 __host__ __device__ __forceinline__ void texel_coords(uint32_t v, uint32_t nl, uint32_t& x, uint32_t& y, uint32_t& z) {
-#if VCT_BRICK2
     const uint32_t nb = nl > 1 ? nl >> 1 : 1u, b = v >> 3;
     x = ((b % nb) << 1) | (v & 1u);
     y = (((b / nb) % nb) << 1) | ((v >> 1) & 1u);
     z = ((b / (nb * nb)) << 1) | ((v >> 2) & 1u);
-#else
-    x = v % nl;
-    y = (v / nl) % nl;
-    z = v / (nl * nl);
-#endif
 }
 
 // level-0 texel of linear-Z voxel v of an n^3 grid (n a power of two)
 __host__ __device__ __forceinline__ uint32_t l0_texel(uint32_t v, uint32_t n) {
-#if VCT_BRICK2
     return texel_index(v & (n - 1u), (v / n) & (n - 1u), v / (n * n), n);
-#else
-    (void)n;
-    return v;
-#endif
 }
 
 __device__ __forceinline__ bool occ_at(const unsigned long long* __restrict__ bits, int n, int x, int y, int z) {

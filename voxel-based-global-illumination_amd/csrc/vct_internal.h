@@ -160,6 +160,14 @@ struct vct_ctx {
     // further device (ranks 1..n-1); empty for a single-device context
     std::vector<vct_ctx*> peers;
     hipEvent_t ev = nullptr;            // cross-device ordering of the multi-device calls
+    // The frame exchanges of trace_multi and vct_comm_trace_frame share scratch slots 8 / 9
+    // (and the peers' streams) whatever stream the caller sets: each such call first makes
+    // the ctx stream wait for the previous call's end (`xchg_done`, recorded on the stream
+    // that call ran on), so frames queued on alternating streams never overlap on the
+    // shared buffers; the event of the last call also covers every earlier one
+    // (vct_comm_synchronize waits for it).
+    hipEvent_t xchg_done = nullptr;
+    hipStream_t xchg_stream = nullptr;
     void* comm = nullptr;               // RCCL communicator of vct_comm_init (ncclComm_t), one process per GPU
     int comm_rank = 0, comm_size = 1;
     uint32_t comm_timeout_ms = 300000;  // deadline of every blocking step of vct_comm_* (vct_comm_set_timeout)
@@ -215,5 +223,9 @@ hipError_t scratch_get(vct_ctx* c, int i, size_t bytes, void** out);
 // K4 scratch `i` (kSc*) of the ctx's current stream, grown to at least `bytes`; *fresh: it
 // was (re)allocated by this call (contents undefined)
 hipError_t k4_scratch(vct_ctx* c, int i, size_t bytes, void** out, bool* fresh);
+// order a frame exchange (shared slot-8 / 9 scratch) after the previous one on any stream,
+// and mark its end (vct_ctx::xchg_done)
+hipError_t xchg_enter(vct_ctx* c);
+hipError_t xchg_leave(vct_ctx* c);
 
 }  // namespace vct

@@ -6,7 +6,7 @@
 // radiance grid; level l >= 2 reads the same face of level l-1.
 //
 // MI355X design: the pyramid is pure HBM streaming.  In the brick layout (vct_device.h
-// VCT_BRICK2) a parent's eight children are one 128-byte brick, and the bricks of a row of
+// texel_index) a parent's eight children are one 128-byte brick, and the bricks of a row of
 // parents are contiguous.  k3_block: a workgroup owns an E^3 block of parents of level l
 // (E = min(8, n_l)) and builds their whole subtree, levels l .. l + log2 E, in LDS:
 //  * its 512 child bricks are staged through LDS with coalesced loads (a wave-instruction
@@ -63,10 +63,9 @@ __device__ __forceinline__ void aniso_faces(const float4 (&ch)[2][2][2], float4 
 
 // children of parent texel (x, y, z) of a level with nc = 2 nl texels per axis:
 // ch[dz][dy][dx] = src[texel of (2x + dx, 2y + dy, 2z + dz)]; in the brick layout
-// (VCT_BRICK2) the eight are one 128-byte brick of the child level
+// the eight are one 128-byte brick of the child level
 __device__ __forceinline__ void load_children(const float4* __restrict__ src, uint32_t x, uint32_t y, uint32_t z,
                                               uint32_t nc, float4 (&ch)[2][2][2]) {
-#if VCT_BRICK2
     const float4* b = src + ((size_t)texel_index(2 * x, 2 * y, 2 * z, nc));
 #pragma unroll
     for (int dz = 0; dz < 2; ++dz)
@@ -74,15 +73,6 @@ __device__ __forceinline__ void load_children(const float4* __restrict__ src, ui
         for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
             for (int dx = 0; dx < 2; ++dx) ch[dz][dy][dx] = b[(dz << 2) | (dy << 1) | dx];
-#else
-#pragma unroll
-    for (int dz = 0; dz < 2; ++dz)
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 2; ++dx)
-                ch[dz][dy][dx] = src[(size_t)(2 * x + dx) + (size_t)nc * ((size_t)(2 * y + dy) + (size_t)nc * (size_t)(2 * z + dz))];
-#endif
 }
 
 // one face of a parent from its children (the k3_levelN operation order)

@@ -6,12 +6,11 @@
 // VoxelizationRenderer::Render (assets/code/renderer/r_voxelization.cpp:4-35).
 //
 // MI355X design (memory-gather bound, no MFMA):
-//  * one lane = one pixel; a 64-lane wave is an 8x8 pixel block, a 256-thread
-//    workgroup a 16x16 block.  The screen is cut into 64x64 tiles; tile t
-//    belongs to rank t % world.  Inside a rank the workgroup ->
-//    tile map is XCD-aware: each of the eight round-robin XCD groups gets one
-//    contiguous run of tiles, so neighbouring blocks (which read the same
-//    bricks) share an L2.
+//  * one lane = one pixel; a 64-lane wave (one workgroup) is an 8x8 pixel
+//    block.  The screen is cut into 64x64 tiles; tile t belongs to rank
+//    t % world.  Inside a rank the workgroup -> tile map is
+//    XCD-aware: whole tiles are dealt to the eight round-robin XCD groups,
+//    so the waves of a tile (which read the same bricks) share an L2.
 //  * The lanes of a wave march the same cone index in lock step.  Diffuse
 //    cones have a wave-uniform step sequence (t, D and the mip pair depend only
 //    on tau), the per-lane early-out (a >= 0.95 / left the grid) just masks the
@@ -108,15 +107,10 @@ __device__ __forceinline__ float lvl_coord(float q, float scale) {
     return fmaf(q, scale, -0.5f);
 }
 
-#ifndef VCT_K4_SLIM
-#define VCT_K4_SLIM 1     // fewer registers held over the march (frame rebuilt per cone, P / n re-read)
-#endif
 // the occupancy form of the default cone trace: 96 VGPRs, 7008 B of LDS (no four-face
-// union), 5 waves/SIMD; the union form keeps VCT_K4_MIN_WAVES (K4Tuner picks per workload)
+// union), 5 waves/SIMD; the union form runs kUnionWaves (K4Tuner picks per workload)
 constexpr int kOccWaves = 5;
-#ifndef VCT_K4_MIN_WAVES
-#define VCT_K4_MIN_WAVES 4      // __launch_bounds__ minimum waves per SIMD of K4 (128 VGPRs)
-#endif
+constexpr int kUnionWaves = 4;  // __launch_bounds__ minimum waves per SIMD (128 VGPRs, 9344 B of LDS)
 
 namespace vct {
 namespace {
@@ -158,12 +152,10 @@ struct TraceK {
     unsigned* spec_state;        // [kSpecSlots] 0 building, 1 ready, 2 needs more than 64 rows
     StepRow* spec_rows;          // [kSpecSlots][64]
     int spec_tabs;               // 0: specular cones always derive their steps per lane (variant bit 0x100)
-    int abl0;                    // always 0 (an SGPR the compiler cannot fold: ablation builds only)
     int split;                   // 0: one workgroup per 16x16 block traces every cone; 1: two (diffuse | specular);
                                  // 2: ndp diffuse parts (cones [g * nd_chunk, ...)) | specular
     int nd_chunk;                // split 2: diffuse cones per part (part g: [g * nd_chunk, (g + 1) * nd_chunk) & nd)
     int ndp;                     // split 2: diffuse parts (>= 2), each followed in blockIdx order by the next
-    int spec_first;              // split 1: the specular part is dispatched first (variant bit 0x2000)
     int xcd_g;                   // units per XCD chunk of the workgroup map (0 = one contiguous run per XCD)
     float4* sc_part;             // split 2: [px] diffuse sum after cones [0, nd_chunk)  (per output index)
     float4* sc_cone;             // split 2: [cone - nd_chunk][px] results of cones [nd_chunk, nd)
@@ -205,10 +197,7 @@ __device__ __forceinline__ float4 combine3(float wx, float wy, float wz, float4 
 }
 
 // corners whose three anisotropic faces are in registers at once (VGPR budget)
-#ifndef VCT_KCH
-#define VCT_KCH 4
-#endif
-constexpr int kCh = VCT_KCH;
+constexpr int kCh = 4;
 // the occupancy form (5 waves/SIMD, 96 VGPRs) keeps 2 corners x 3 faces in flight
 constexpr int kChOcc = 2;
 template <bool UNION> constexpr int gather_chunk() { return UNION ? kCh : kChOcc; }
@@ -236,44 +225,25 @@ struct LevelView<true> {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, in ? i << 4 : 0xfffffff0u, 0, 0);
         return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
     }
-    // ablation: the same load again (soffset = an opaque 0), its value kept alive unused
-    __device__ void twin(uint32_t i, bool in, int z) const {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, in ? i << 4 : 0xfffffff0u, z, 0);
-        asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
-    }
 };
 
 template <>
 struct LevelView<false> {
     const float4* p;
-    __device__ void twin(uint32_t, bool, int) const {}
     __device__ float4 fetch(uint32_t i, bool in) const {
         const float4 v = p[in ? i : 0u];
         return sel4(in, v, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     }
 };
 
-// level l (wave-uniform): O32 takes the level's texel offset from the kernel-argument
-// table (one scalar load; measured 0.7-0.9 % faster than deriving it on the scalar unit,
-// which also held ~34 more SGPRs) and its size from shifts (n a power of two)
-// level views from the host's per-level base / size table (1) or derived per view (0)
-#ifndef VCT_K4_LVLTAB
-#define VCT_K4_LVLTAB 1
-#endif
+// level l (wave-uniform): O32 takes the level's base and size from the host's per-level
+// table in the kernel arguments (launch_trace; one scalar load per level view, measured
+// faster than deriving them on the scalar unit, which also held ~34 more SGPRs)
 template <bool O32>
 __device__ __forceinline__ LevelView<O32> level_view(const TraceK& k, int l) {
     if constexpr (O32) {
-#if VCT_K4_LVLTAB
-        // base and size precomputed per level on the host (launch_trace)
         const LevelRange r = k.lvl[l];
         return LevelView<true>{__builtin_amdgcn_make_buffer_rsrc((void*)r.base, (short)0, (int)r.bytes, 0x00020000)};
-#else
-        const uint32_t lg = (uint32_t)k.lgn, F = k.aniso ? 6u : 1u;
-        const uint32_t off = (uint32_t)k.lvl_off[l];   // < 2^31 texels for n <= 512
-        const uint32_t bytes = (l == 0 ? 1u : F) << (3u * (lg - (uint32_t)l) + 4u);
-        return LevelView<true>{__builtin_amdgcn_make_buffer_rsrc((void*)(k.pyr + off), (short)0, (int)bytes,
-                                                                 0x00020000)};
-#endif
     } else {
         return LevelView<false>{k.pyr + k.lvl_off[l]};
     }
@@ -333,14 +303,6 @@ __device__ __forceinline__ float4 sample_level_bits(const TraceK& k, int l, floa
     for (int c = 0; c < 8; ++c) off[c] = (c & 1 ? X.t1 : X.t0) | ((c >> 1) & 1 ? Y.t1 : Y.t0) | (c >> 2 ? Z.t1 : Z.t0);
     const LevelView<true> lv = level_view<true>(k, l);
     const auto ld = [&](uint32_t o) {
-#ifdef VCT_ABL_GATHER
-        // ablation: the same load again (soffset = an opaque 0), its value kept alive unused;
-        // VCT_ABL_GATHER = 1 every lane, 2 one lane of each 2x2 pixel quad, 3 the first 16 lanes
-        if (VCT_ABL_GATHER == 1 || (VCT_ABL_GATHER == 2 ? (threadIdx.x & 3) == 0 : (threadIdx.x & 63) < 16)) {
-            const auto w = __builtin_amdgcn_raw_buffer_load_b128(lv.r, o, k.abl0, 0);
-            asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]));
-        }
-#endif
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(lv.r, o, 0, 0);
         return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
     };
@@ -376,9 +338,7 @@ __device__ __forceinline__ float4 sample_level_bits(const TraceK& k, int l, floa
 template <bool O32, bool UNIF = false, int KC = kCh>   // UNIF: l wave-uniform (buffer resource); else per lane
 __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx, float qy, float qz,
                                                int fx, int fy, int fz, float wdx, float wdy, float wdz) {
-#if VCT_BRICK2
     if constexpr (O32 && UNIF) return sample_level_bits<KC>(k, l, qx, qy, qz, fx, fy, fz, wdx, wdy, wdz);
-#endif
     const float scale = __uint_as_float((uint32_t)(127 - l) << 23);  // 2^-l, exact
     const int nl = k.n >> l;
     const float cx = lvl_coord(qx, scale), cy = lvl_coord(qy, scale), cz = lvl_coord(qz, scale);
@@ -389,7 +349,6 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
     uint32_t idx[8];
     bool in[8];
     const int xs[2] = {ix, ix + 1}, ys[2] = {iy, iy + 1}, zs[2] = {iz, iz + 1};
-#if VCT_BRICK2
     // brick layout (vct_device.h texel_index), per-axis terms: corner index = X + Y + Z.
     // 24-bit multiplies (v_mul_lo_u32 is quarter rate) where every in-range term fits
     // (n <= 512: (z >> 1) nb^2 < 2^24); an out-of-range corner's index is never read
@@ -408,34 +367,11 @@ __device__ __forceinline__ float4 sample_level(const TraceK& k, int l, float qx,
         in[c] = (unsigned)x < (unsigned)nl && (unsigned)y < (unsigned)nl && (unsigned)z < (unsigned)nl;
         idx[c] = tx[c & 1] + ty[(c >> 1) & 1] + tz[c >> 2];
     }
-#else
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const int x = xs[c & 1], y = ys[(c >> 1) & 1], z = zs[c >> 2];
-        in[c] = (unsigned)x < (unsigned)nl && (unsigned)y < (unsigned)nl && (unsigned)z < (unsigned)nl;
-        // 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate): nl <= 512 and y + nl z < 2^18
-        // for every in-range corner; an out-of-range corner's index is never read (in[c] = false)
-        idx[c] = (uint32_t)x + __umul24((uint32_t)nl, (uint32_t)y + __umul24((uint32_t)nl, (uint32_t)z));
-    }
-#endif
     const auto lv = [&] {
         if constexpr (UNIF) return level_view<O32>(k, l);
         else return level_view_lane(k, l);
     }();
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#ifdef VCT_ABL_GATHER
-    if constexpr (UNIF) {
-        const uint32_t vl0 = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            lv.twin(idx[c], in[c], k.abl0);
-            if (l > 0 && k.aniso) {
-                lv.twin((uint32_t)fy * vl0 + idx[c], in[c], k.abl0);
-                lv.twin((uint32_t)fz * vl0 + idx[c], in[c], k.abl0);
-            }
-        }
-    }
-#endif
     if (l == 0 || !k.aniso) {
         float4 v[8];
 #pragma unroll
@@ -532,25 +468,9 @@ __device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, f
 // every z step onto the same banks.
 constexpr int kBz = 19;
 constexpr int kBlk = 3 * kBz + 16;              // one face block: 73 slots
-// four-face cones in the occupancy form (VCT_K4_F43): 4 x 4 x 3 bricks, four 54-slot
-// face blocks (216 slots) in the 219-slot entry
-#ifndef VCT_K4_F43
-#define VCT_K4_F43 1
-#endif
+// four-face cones in the occupancy form: 4 x 4 x 3 bricks, four 54-slot face blocks
+// (216 slots) in the 219-slot entry
 constexpr int kBlk3 = 2 * kBz + 16;
-// the two-level test of table rows on the scalar unit from fr's bits (1)
-#ifndef VCT_K4_TWOS
-#define VCT_K4_TWOS 1
-#endif
-// brick origin counts from the SCC of the masking s_and_b64 (1) or s_cmp / s_cselect (0)
-#ifndef VCT_K4_ORIGIN_SCC
-#define VCT_K4_ORIGIN_SCC 1
-#endif
-// a step that restages one level runs a staging copy per level (1) instead of selecting
-// the level, mode and origin between the two (0)
-#ifndef VCT_K4_STSPLIT
-#define VCT_K4_STSPLIT 1
-#endif
 // float4 slots per cache entry: up to 4 face blocks (3 without the four-face union)
 // The two cache entries live in LDS regions 0 and 1 (entry a in region `flip`): 9344 B
 // per wave with the union (4 waves/SIMD fit the 160 KB), 7008 B without (5 waves/SIMD).
@@ -561,12 +481,7 @@ template <bool UNION> constexpr int lds_slots() { return 2 * entry_slots<UNION>(
 // writes): the asm "memory" clobber keeps the compiler from moving DS ops
 // across it, lgkmcnt(0) makes it explicit in hardware.
 __device__ __forceinline__ void wave_lds_sync() {
-#ifdef VCT_LDS_NOWAIT
-    // LDS instructions of one wave execute in order: a compiler fence suffices
-    asm volatile("" ::: "memory");
-#else
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -625,28 +540,16 @@ __device__ __forceinline__ bool in_brick(const Corner& c, const BrickEntry& b, i
 // negb = 0 or 1 (the cone moves toward -axis): integer arithmetic on wave-uniform values
 // only, so the origin stays on the scalar unit (a `neg ? :` on a bool is lowered as a
 // lane mask and drags the origin into VGPRs)
-// (m != 0) as an SGPR integer: LLVM lowers a uniform i1 to a lane mask and would
-// finish the origin arithmetic on the VALU (v_cndmask / v_addc / v_mul_lo)
-__device__ __forceinline__ int s_nonzero(unsigned long long m) {
-    int r;
-    asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(m) : "scc");
-    return r;
-}
 __device__ __forceinline__ int wave_origin(int v, unsigned long long am, int fl, int negb, int back = 2) {
     const int b = __builtin_amdgcn_readlane(v, fl);
     const int sg = 1 - 2 * negb;                       // +1 / -1
     const int sv = __mul24(v, sg), sb = b * sg;        // mirrored toward -axis
-#if VCT_K4_ORIGIN_SCC
     // cnt = (m1 & am != 0) + (m2 & am != 0) from the SCC that s_and_b64 sets (4 scalar
     // instructions instead of two masks, two compare / select pairs and an add)
     unsigned long long m2 = wballot(sv < sb - 1), m1 = wballot(sv < sb);   // m2 within m1
     int cnt;
     asm("s_and_b64 %1, %1, %3\n\ts_cselect_b32 %0, 1, 0\n\ts_and_b64 %2, %2, %3\n\ts_addc_u32 %0, %0, 0"
         : "=&s"(cnt), "+s"(m1), "+s"(m2) : "s"(am) : "scc");
-#else
-    const unsigned long long m2 = wballot(sv < sb - 1) & am, m1 = wballot(sv < sb) & am;   // m2 within m1
-    const int cnt = s_nonzero(m1) + s_nonzero(m2);
-#endif
     return b - sg * cnt - back * negb;      // back = brick depth - 2
 }
 
@@ -685,14 +588,6 @@ __device__ __forceinline__ Tex4 stage_load(const TraceK& k, int l, const BrickEn
     const LevelView<O32> lv = level_view<O32>(k, l);
     Tex4 t;
     t.b = t.c = t.d = z4;
-#ifdef VCT_ABL_STAGE
-    lv.twin(gi, inb, k.abl0);
-    if (mode != kIso) {
-        const uint32_t vl0 = (uint32_t)nl * (uint32_t)nl * (uint32_t)nl;
-        lv.twin((uint32_t)cc.f1 * vl0 + gi, inb, k.abl0);
-        lv.twin((uint32_t)cc.f2 * vl0 + gi, inb, k.abl0);
-    }
-#endif
     if (mode == kIso) {
         t.a = lv.fetch(gi, inb);
     } else {
@@ -834,7 +729,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const int aniso_mode = AM >= 0 ? AM : (cc.dir_uniform ? kComb : kFaces);
     const int modeA = (l0 == 0 || !k.aniso) ? kIso : aniso_mode;
     const int modeB = k.aniso ? aniso_mode : kIso;
-    const bool faces_ok = AM == kComb || (UNION || VCT_K4_F43 ? cc.nfaces <= 4 : cc.nfaces == 3);
+    const bool faces_ok = AM == kComb || cc.nfaces <= 4;
     // faces-mode levels of a four-face cone in the occupancy form: 4 x 4 x 3 bricks
     // (a dir_uniform cone has three faces: never z3)
     const int z3A = AM != kComb && modeA == kFaces ? cc.z3 : 0, z3B = AM != kComb && modeB == kFaces ? cc.z3 : 0;
@@ -894,25 +789,14 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
         bA.zero = bc.a.zero = wall(zA);
         bB.zero = bc.b.zero = wall(zB);
         wave_lds_sync();
-    } else if (VCT_K4_STSPLIT && stA) {
+    } else if (stA) {      // one level restages: a staging copy per level (no selects between the two)
         bA.zero = bc.a.zero = wall(stage_store<AM>(modeA, cc, stage_load<O32, AM>(k, l0, bA, modeA, cc), ldsA));
         wave_lds_sync();
-    } else if (VCT_K4_STSPLIT && stB) {
+    } else if (stB) {
         bB.zero = bc.b.zero = wall(stage_store<AM>(modeB, cc, stage_load<O32, AM>(k, l1, bB, modeB, cc), ldsB));
-        wave_lds_sync();
-    } else if (stA || stB) {
-        const int mode = stA ? modeA : modeB;
-        const bool z = wall(stage_store<AM>(mode, cc, stage_load<O32, AM>(k, stA ? l0 : l1, stA ? bA : bB, mode, cc),
-                                        stA ? ldsA : ldsB));
-        if (stA) bA.zero = bc.a.zero = z;
-        else bB.zero = bc.b.zero = z;
         wave_lds_sync();
     }
     pc.mark(2);
-#ifndef VCT_K4_PRIO
-#define VCT_K4_PRIO 0   // round 2: without it 0.3-0.7 % faster (A/B); 3 = the round-1 placement
-#endif
-    if (VCT_K4_PRIO) __builtin_amdgcn_s_setprio(VCT_K4_PRIO);   // LDS sampling / FMAs issue ahead of other waves (A/B: -0.6 %)
     float4 sA = z4, sB = z4;
     const bool readA = useA && !bA.zero, readB = useB && !bB.zero;
     if (useA) VCT_DBG(bA.zero ? 17 : 15);          // level-A samples from zero / nonzero bricks
@@ -1009,42 +893,6 @@ __device__ __forceinline__ bool spec_table(const TraceK& k, float tau, unsigned 
     return false;
 }
 
-// Ablation builds (perturbation measurements, never the product): extra work per
-// wave-step whose results are kept alive but never used, to measure how the
-// kernel time responds to more VALU / SALU issue (VCT_ABL_VALU / VCT_ABL_SALU =
-// instructions per wave-step).  VCT_ABL_GATHER / VCT_ABL_STAGE / VCT_ABL_LDS
-// issue every per-lane gather / staging load / LDS sample read twice.
-__device__ __forceinline__ int vct_abl_zero() {
-    int z;
-    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-    return z;
-}
-__device__ __forceinline__ void ablate_step(int i) {
-#if defined(VCT_ABL_VALU) && VCT_ABL_VALU > 0
-    float d0 = (float)i, d1 = d0, d2 = d0, d3 = d0;
-#pragma unroll
-    for (int j = 0; j < VCT_ABL_VALU / 4; ++j)
-        asm volatile("v_add_f32 %0, 1.0, %0\n v_add_f32 %1, 1.0, %1\n v_add_f32 %2, 1.0, %2\n v_add_f32 %3, 1.0, %3"
-                     : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
-    asm volatile("" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3));
-#endif
-#if defined(VCT_ABL_SALU)
-    (void)i;
-    int s0 = __builtin_amdgcn_readfirstlane(vct_abl_zero()), s1 = s0 + 3;   // not tied to the loop counter
-#pragma unroll
-    for (int j = 0; j < VCT_ABL_SALU / 2; ++j)
-        asm volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 3" : "+s"(s0), "+s"(s1) : : "scc");
-    asm volatile("" ::"s"(s0), "s"(s1));
-#endif
-#if defined(VCT_ABL_NOP)
-#pragma unroll
-    for (int j = 0; j < VCT_ABL_NOP; ++j) asm volatile("s_nop 0");
-#endif
-#if defined(VCT_ABL_SLEEP)
-    __builtin_amdgcn_s_sleep(VCT_ABL_SLEEP);
-#endif
-}
-
 // one cone, wave-synchronous (A.6); same arithmetic as march().  TAB: (t, D,
 // l0, fr) come from a step table (the diffuse one, or a specular one).  CNT:
 // count steps and texel fetches (the launches that report them); else both stay 0.
@@ -1091,16 +939,17 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
         // same d^2 everywhere AND one face per axis (d and -d share d^2)
         cc.dir_uniform = wall_in(vm, (wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz)) && cc.nfaces == 3;
-        cc.z3 = !UNION && VCT_K4_F43 && cc.nfaces == 4 ? 1 : 0;
+        cc.z3 = !UNION && cc.nfaces == 4 ? 1 : 0;
         cc.bstr = cc.z3 ? kBlk3 : kBlk;
     }
     BrickCache bc;
     bc.a = bc.b = BrickEntry{-1, 0, 0, 0, 0};
     bc.flip = 0;
-    // The march is compiled once per anisotropic staging mode (VCT_K4_AMSPEC): a
-    // dir_uniform cone (flat surfaces) stages combined faces at every anisotropic level,
-    // any other cone stages face blocks, so the per-step mode selects, the four-face /
-    // z3 tests and the faces-mode sampling fold away in the combined-face copy.
+    // The table marches are compiled once per anisotropic staging mode: a dir_uniform
+    // cone (flat surfaces) stages combined faces at every anisotropic level, any other
+    // cone stages face blocks, so the per-step mode selects, the four-face / z3 tests
+    // and the faces-mode sampling fold away in the combined-face copy.  (Specialising
+    // the per-lane specular march too measured slower: -1.0 % instead of -1.6 %.)
     auto march_loop = [&](auto am_tag) __attribute__((always_inline)) {
     constexpr int AM = decltype(am_tag)::value;
     for (int i = 0;; ++i) {
@@ -1130,7 +979,6 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         VCT_DBG(TAB ? 36 : 38);                               // wave-steps (table / per-lane steps)
         VCT_DBGN(37, __builtin_popcountll(am));               // active lanes over those wave-steps
         VCT_DBGN(39, __builtin_popcountll(wballot(valid)));   // lanes holding a valid pixel
-        ablate_step(i);
         if constexpr (!TAB) {
             D = fmaxf(1.0f, tau2 * t);
             float m = spec_log2(D);
@@ -1141,21 +989,16 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         // both levels sampled: fr > 0 (fr >= +0 here, so a nonzero bit pattern) and l0 < L;
         // for table rows both are wave-uniform: a scalar test, no VALU compare and ballot
         unsigned long long two_m;
-#if VCT_K4_TWOS
         // on the scalar unit from fr's bits (LLVM otherwise turns the bit test into a VALU class test)
         if constexpr (TAB)
             asm("s_cmp_lg_u32 %1, 0\n\ts_cselect_b64 %0, -1, 0\n\ts_cmp_lt_i32 %2, %3\n\ts_cselect_b64 %0, %0, 0"
                 : "=&s"(two_m) : "s"(frb), "s"(l0), "s"(k.L) : "scc");
-#else
-        if constexpr (TAB) two_m = ((__float_as_uint(fr) != 0u) & (l0 < k.L)) ? ~0ull : 0ull;
-#endif
         else two_m = wballot(fr > 0.0f) & wballot(l0 < k.L);
         const bool two = __builtin_amdgcn_inverse_ballot_w64(two_m);
         const int l0f = TAB ? l0 : __builtin_amdgcn_readlane(l0, __builtin_ctzll(am));
         float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (TAB || wall_in(am, l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
-            if (VCT_K4_PRIO) __builtin_amdgcn_s_setprio(0);   // default priority for the step head, brick geometry and staging
             s = step_bricks<O32, UNION, KL, AM>(k, l0f, qx, qy, qz, am, am & two_m, fr, cc, ld, lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
             s = sample_level<O32, false, gather_chunk<UNION>()>(k, l0, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(),
@@ -1184,13 +1027,8 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         pc.mark(5);
     }
     };
-#ifndef VCT_K4_AMSPEC
-#define VCT_K4_AMSPEC 2
-#endif
-    // 1: every march; 2: the table marches only
-    constexpr bool kAmSpec = VCT_K4_AMSPEC == 1 || (VCT_K4_AMSPEC == 2 && TAB);
-    if (kAmSpec && cc.dir_uniform) march_loop(std::integral_constant<int, kComb>{});
-    else if (kAmSpec) march_loop(std::integral_constant<int, kFaces>{});
+    if (TAB && cc.dir_uniform) march_loop(std::integral_constant<int, kComb>{});
+    else if (TAB) march_loop(std::integral_constant<int, kFaces>{});
     else march_loop(std::integral_constant<int, -1>{});
     res = make_float4(cr, cg, cb, a);
     return steps;
@@ -1218,14 +1056,15 @@ __device__ __forceinline__ float4 ld_coherent(float4* p) {
 // ===========================================================================
 // the kernel: pixel setup, cone loop, outputs (BRICK = variant 0, else 1)
 // ===========================================================================
-// S3: the split-2 instantiation.  WG1: one wave per workgroup (an 8x8 block): a
-// wave's LDS is released when that wave ends, not when the slowest of four has
-// CNT: the launch reports step / texel counts (steps_px, cone_steps, texel_fetches);
-// the timed frame loop passes none and runs the form without the counting VALU.
-template <bool BRICK, int MINW, bool UNION, bool O32, int KL = 2, bool MORTON = true, bool S3 = false,
-          bool WG1 = true, bool CNT = true>
-__global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
-    __shared__ float4 lds_all[BRICK && !WG1 ? 4 : 1][BRICK ? lds_slots<UNION>() : 1];
+// One wave per workgroup (an 8x8 block): a wave's LDS is released when that wave
+// ends (measured: four waves per workgroup held it until the slowest of four ended).
+// S3: the split-2 instantiation.  CNT: the launch reports step / texel counts
+// (steps_px, cone_steps, texel_fetches); the timed frame loop passes none and runs
+// the form without the counting VALU.
+constexpr int kKL = 2;    // corners x 3 faces per LDS burst in faces mode (1 / 4 measured slower)
+template <bool BRICK, int MINW, bool UNION, bool O32, bool S3 = false, bool CNT = true>
+__global__ void __launch_bounds__(64, MINW) k4_trace(TraceK k) {
+    __shared__ float4 lds[BRICK ? lds_slots<UNION>() : 1];
     // split: the grid is 2 or 3 parts over the same pixels, dispatched in
     // blockIdx order: split 1 = diffuse cones | specular cone; split 2 = diffuse
     // cones [0, c) | [c, 2c) | ... | specular (ndp diffuse parts of c = nd_chunk cones;
@@ -1238,9 +1077,9 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     const uint32_t nb = S3 ? gridDim.x / (uint32_t)(k.ndp + 1) : (k.split ? gridDim.x >> 1 : gridDim.x);
     const uint32_t part = S3 ? blockIdx.x / nb : (blockIdx.x >= nb ? 1u : 0u);
     const uint32_t b = blockIdx.x - part * nb;
-    // XCD-aware workgroup -> (local tile, 16x16 block) map, bijective for any grid.
-    // The hardware hands workgroup b to XCD b & 7.  Units (waves with WG1, else
-    // 16x16 blocks) are dealt to the XCDs in chunks of G consecutive units (the
+    // XCD-aware workgroup -> (local tile, 8x8 block) map, bijective for any grid.
+    // The hardware hands workgroup b to XCD b & 7.  Units (waves) are dealt to the
+    // XCDs in chunks of G consecutive units (the
     // pixels of a chunk share that XCD's L2), chunk c to XCD c & 7, so every XCD
     // gets a screen-wide sample of the frame: cost varies strongly across the
     // image (the atrium's middle rows cost ~2x its top and bottom rows), and
@@ -1257,13 +1096,13 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
         const uint32_t kk = b >> 3;
         rbw = b < full ? G * (xcd + 8u * (kk / G)) + kk % G : b;
     }
-    const uint32_t rb = WG1 ? rbw >> 2 : rbw;                 // the 16x16 block
-    const uint32_t wave = WG1 ? (rbw & 3u) : threadIdx.x >> 6;  // its 8x8 quarter
+    const uint32_t rb = rbw >> 2;                 // the 16x16 block
+    const uint32_t wave = rbw & 3u;               // its 8x8 quarter
     const uint32_t lt = rb >> 4, sub = rb & 15;
     int c_lo = 0, c_hi = k.nd, grp = 0;        // diffuse cones [c_lo, c_hi); grp g >= 1: diffuse part g - 1 of split 2
     bool do_spec = k.spec_on != 0, wr_diff = true, wr_spec = true;
     if (k.split == 1) {
-        if ((part == 0) != (k.spec_first != 0)) { do_spec = false; wr_spec = false; }
+        if (part == 0) { do_spec = false; wr_spec = false; }
         else { c_hi = 0; wr_diff = false; }
     } else if (S3) {
         if (part == (uint32_t)k.ndp) { c_hi = 0; wr_diff = false; }
@@ -1272,16 +1111,16 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
     }
     const bool do_diff = c_hi > c_lo;
     const uint32_t lane = threadIdx.x & 63;
-    float4* lds = lds_all[BRICK && !WG1 ? wave : 0];
     PhaseClock pc;
     pc.start();
 #if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
     const unsigned long long wave_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    // lane -> pixel of the wave's 8x8 block in Morton order (MORTON; else row-major):
-    // the lanes of each ds_read_b128 / load group are then a compact 2x2 / 4x4 pixel block
-    const uint32_t mx = MORTON ? (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4) : lane & 7;
-    const uint32_t my = MORTON ? ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4) : lane >> 3;
+    // lane -> pixel of the wave's 8x8 block in Morton order: the lanes of each
+    // ds_read_b128 / load group are then a compact 2x2 / 4x4 pixel block (measured
+    // against row-major lanes: 2.07 -> 1.92 ms in round 1)
+    const uint32_t mx = (lane & 1) | ((lane >> 1) & 2) | ((lane >> 2) & 4);
+    const uint32_t my = ((lane >> 1) & 1) | ((lane >> 2) & 2) | ((lane >> 3) & 4);
     const uint32_t px = (sub & 3) * 16 + (wave & 1) * 8 + mx;
     const uint32_t py = (sub >> 2) * 16 + (wave >> 1) * 8 + my;
     bool in_frame;
@@ -1322,11 +1161,9 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
         const float oz = (P.z - k.g0z) * k.inv_h + nz;
         const float(*cones)[4] = cone_table(k.nd);
         for (int c = S3 ? c_lo : 0; c < c_hi; ++c) {
-#if VCT_K4_SLIM
             // the tangent frame is rebuilt per cone (a few VALU per ~12 steps) instead of
             // holding 6 VGPRs over the march; the empty asm keeps LLVM from hoisting it
             asm volatile("" : "+v"(nx), "+v"(ny), "+v"(nz));
-#endif
             // Duff et al. 2017 branchless orthonormal basis
             const float sgn = copysignf(1.0f, nz);
             const float ka = -1.0f / (sgn + nz);
@@ -1338,7 +1175,7 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
             const float dy = (cn * ny + ct * Ty) + cb * By;
             const float dz = (cn * nz + ct * Tz) + cb * Bz;
             float4 res;
-            if constexpr (BRICK) steps += march_brick<O32, UNION, true, KL, CNT>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, tab, pc);
+            if constexpr (BRICK) steps += march_brick<O32, UNION, true, kKL, CNT>(k, valid, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels, lds, tab, pc);
             else steps += march<O32>(k, ox, oy, oz, dx, dy, dz, k.tau_d, res, texels);
             if (S3 && grp >= 2) {                // later parts: results go to the hand-over scratch
                 if (in_frame || k.compact) st_coherent(&k.sc_cone[(size_t)(c - k.nd_chunk) * k.sc_px + oidx], res);
@@ -1350,19 +1187,13 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
             }
         }
         dout = sel4(valid, make_float4(ir, ig, ib, 1.0f - occ), dout);
-#ifndef VCT_EXP_NOSPEC
         if (do_spec) {
-#else
-        if (false) {
-#endif
-#if VCT_K4_SLIM
             // position and normal are read again rather than held over the diffuse march
             // (the compiler fence keeps the loads from being merged with the first ones)
             asm volatile("" ::: "memory");
             if (in_frame) P = k.pos[pix];
             if (valid) N4 = k.nrm[pix];
             nx = N4.x; ny = N4.y; nz = N4.z;
-#endif
             float vx = k.ex - P.x, vy = k.ey - P.y, vz = k.ez - P.z;
             float vl = sqrtf(dot3(vx, vy, vz, vx, vy, vz));
             vl = valid ? vl : 1.0f;
@@ -1376,9 +1207,9 @@ __global__ void __launch_bounds__(WG1 ? 64 : 256, MINW) k4_trace(TraceK k) {
             float4 res;
             if constexpr (BRICK) {
                 if (spec_table(k, tau, wballot(valid), tab))
-                    steps += march_brick<O32, UNION, true, KL, CNT>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
+                    steps += march_brick<O32, UNION, true, kKL, CNT>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
                 else
-                    steps += march_brick<O32, UNION, false, KL, CNT>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
+                    steps += march_brick<O32, UNION, false, kKL, CNT>(k, valid, ox, oy, oz, rx, ry, rz, tau, res, texels, lds, tab, pc);
             } else {
                 steps += march<O32>(k, ox, oy, oz, rx, ry, rz, tau, res, texels);
             }
@@ -1657,14 +1488,12 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.spec_state = c->spec_keys + kSpecSlots;
     k.spec_rows = c->spec_rows;
     k.spec_tabs = (a->variant & 0x100) ? 0 : 1;
-    k.abl0 = 0;
     // cone groups in separate workgroups (variant bits: 0x200 off, 0x400 three parts,
     // 0x800 two parts; default by launch size); per-pixel step counts need every
     // cone of a pixel in one lane, so steps_px keeps one part
     k.split = (k.spec_on && k.nd > 0 && !a->steps_px && !(a->variant & 0x200)) ? 1 : 0;
     k.nd_chunk = (k.nd + 1) / 2;
     k.ndp = 2;
-    k.spec_first = (a->variant & 0x2000) ? 1 : 0;
     {   // variant bits 16-19: XCD map (0 default; 1 contiguous runs; 2..6: chunks of 1, 4, 16, 64, 256 units)
         static const int g_of[7] = {0, 0, 1, 4, 16, 64, 256};
         const uint32_t m = (a->variant >> 16) & 0xf;
@@ -1673,6 +1502,8 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.sc_part = k.sc_cone = nullptr; k.sc_flag = nullptr; k.sc_px = 0;
     k.perm = nullptr;
     k.npx = a->width * a->height;
+    // low byte: 0 default, 1 per-lane gathers; the other variant bits of vct_variants.h
+    if ((a->variant & 0xfe) != 0 || (a->variant & kVarRetired) != 0) return hipErrorInvalidValue;
     uint32_t nlt = tiles_for_rank(a->width, a->height, (uint32_t)k.rank, world);
     if (nlt == 0) return hipSuccess;
     const bool counting = k.steps_px || k.steps_total || k.texels_total;
@@ -1682,7 +1513,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     // reordering only when 0x8000 asks for it.
     const bool deflt = (a->variant & 0xff) == 0;
     const bool can_reorder = world == 1 && !k.compact;
-    const bool cnt_form = counting || (a->variant & 0x1000) || (a->variant & 0x4000);   // 0x1000: four waves per workgroup
+    const bool cnt_form = counting || (a->variant & kVarCountingForm);
     int cand = 0;
     hipEvent_t* ev = nullptr;
     {
@@ -1717,7 +1548,6 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         if (e != hipSuccess) return e;
         nlt = (k.npx + 64u * 64u - 1u) / (64u * 64u);
     }
-    const bool wg1 = !(a->variant & 0x1000);    // 0x1000: four waves per workgroup
     uint32_t blocks = nlt * 16;
     if (k.split && k.nd > 1 && ((a->variant & 0x400) || (!(a->variant & 0x800) && blocks <= kSplit3MaxBlocks))) {
         // ndp diffuse parts + the specular part (ndp = 2 unless variant bits 20-23 ask for
@@ -1745,49 +1575,34 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         k.sc_px = npx;
     }
     const uint32_t nparts = k.split == 2 ? (uint32_t)k.ndp + 1u : 1u + (uint32_t)k.split;
-    blocks *= nparts;
-    const uint32_t wgs = wg1 ? 64u : 256u;
-    if (wg1) blocks *= 4u;
+    blocks *= nparts * 4u;                       // one wave (8x8 block) per workgroup
     if (((a->variant >> 16) & 0xf) == 0) {
         // default XCD chunk: whole 64x64 tiles (64 waves) for full frames; 64x16 strips
         // for the small launches of a multi-GPU rank (measured: 1080p 1.60 -> 1.44 ms,
         // 4K 6.91 -> 6.15 ms, one rank of 8: 0.288 -> 0.265 ms)
-        const uint32_t units_per_part = blocks / nparts;
-        const uint32_t unit_g = wg1 ? 1u : 4u;      // a 16x16 block is 4 waves
-        k.xcd_g = (int)((units_per_part * unit_g >= 16384u ? 64u : 16u) / unit_g);
+        k.xcd_g = blocks / nparts >= 16384u ? 64 : 16;
     }
     // O32 instantiations need every level below 4 GiB: n <= 512
     const bool o32 = g.n <= 512;
-#define VCT_K4_WG(BRICK, MINW, UNION, WG, CNT)                                                          \
+#define VCT_K4(BRICK, MINW, UNION, CNT)                                                                 \
     do {                                                                                               \
         if (k.split == 2) {                                                                            \
-            if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, true, WG, CNT>), dim3(blocks), dim3(wgs), 0, c->stream, k); \
-            else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, true, WG, CNT>), dim3(blocks), dim3(wgs), 0, c->stream, k);   \
-        } else if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, 2, true, false, WG, CNT>), dim3(blocks), dim3(wgs), 0, c->stream, k); \
-        else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, 2, true, false, WG, CNT>), dim3(blocks), dim3(wgs), 0, c->stream, k);    \
+            if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, true, CNT>), dim3(blocks), dim3(64), 0, c->stream, k); \
+            else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, true, CNT>), dim3(blocks), dim3(64), 0, c->stream, k);   \
+        } else if (o32) hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, true, false, CNT>), dim3(blocks), dim3(64), 0, c->stream, k); \
+        else hipLaunchKernelGGL((k4_trace<BRICK, MINW, UNION, false, false, CNT>), dim3(blocks), dim3(64), 0, c->stream, k);    \
     } while (0)
-#define VCT_K4(BRICK, MINW, UNION)                                                                      \
-    do {                                                                                               \
-        if (wg1) VCT_K4_WG(BRICK, MINW, UNION, true, true);                                            \
-        else VCT_K4_WG(BRICK, MINW, UNION, false, true);                                               \
-    } while (0)
-    switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers; 2 bricks without the four-face union
-        case 1: VCT_K4(false, 1, true); break;
-        case 2: VCT_K4(true, VCT_K4_MIN_WAVES, false); break;
-        case 3:   // row-major lanes (one wave per workgroup only)
-            if (!wg1) return hipErrorInvalidValue;
-            if (k.split == 2) hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false, true>), dim3(blocks), dim3(wgs), 0, c->stream, k);
-            else hipLaunchKernelGGL((k4_trace<true, VCT_K4_MIN_WAVES, true, true, 2, false>), dim3(blocks), dim3(wgs), 0, c->stream, k);
-            break;
+    switch (a->variant & 0xff) {   // 0 default; 1 per-lane gathers
+        case 1: VCT_K4(false, 1, true, true); break;
         default: {
             // 0x4000: the counting form without counters; the form is the candidate's bit 0
             const int form = cand & 1;
             if (cnt_form) {
-                if (form) VCT_K4(true, kOccWaves, false);
-                else VCT_K4(true, VCT_K4_MIN_WAVES, true);
+                if (form) VCT_K4(true, kOccWaves, false, true);
+                else VCT_K4(true, kUnionWaves, true, true);
             } else {
-                if (form) VCT_K4_WG(true, kOccWaves, false, true, false);
-                else VCT_K4_WG(true, VCT_K4_MIN_WAVES, true, true, false);
+                if (form) VCT_K4(true, kOccWaves, false, false);
+                else VCT_K4(true, kUnionWaves, true, false);
             }
             if (ev) (void)hipEventRecord(ev[1], c->stream);
             K4Tuner& T = c->k4tune;
@@ -1797,7 +1612,6 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         }
     }
 #undef VCT_K4
-#undef VCT_K4_WG
     return hipGetLastError();
 }
 

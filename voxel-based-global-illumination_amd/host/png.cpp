@@ -36,6 +36,9 @@ int paeth(int a, int b, int c) {
 }
 
 bool inflate_all(const std::vector<uint8_t>& in, size_t want, std::vector<uint8_t>* out, std::string* err) {
+    // deflate expands at most 1032:1 (a 258-byte match per ~2 bits): a stream too short
+    // for the declared image fails here instead of sizing a buffer from the header alone
+    if (want / 1032u > in.size() + 64u) return fail(err, "png: not enough pixels");
     out->assign(want, 0);
     z_stream z;
     std::memset(&z, 0, sizeof z);
@@ -88,6 +91,13 @@ bool DecodePng(const uint8_t* f, size_t n, PngImage* out, std::string* err) {
                     (color != 0 && color != 3 && depth < 8))
                     return fail(err, "png: bad colour type");
                 if (d[10] != 0 || d[11] != 0 || interlace > 1) return fail(err, "png: bad compression / filter / interlace");
+                {
+                    // stb_image's limit (stb_image.h:4837-4845): at most 2^30 bytes of decoded
+                    // image, counted at the file's channel count (4 for a palette image, whose
+                    // pixels expand to RGBA); checked before any buffer is sized from w and h
+                    const uint32_t cn = color == 3 ? 4u : (uint32_t)((color & 2 ? 3 : 1) + (color & 4 ? 1 : 0));
+                    if ((1u << 30) / w / cn < h) return fail(err, "png: too large");
+                }
                 first = false;
                 break;
             case 0x504c5445u:   // PLTE

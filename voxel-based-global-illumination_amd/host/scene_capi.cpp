@@ -1,7 +1,9 @@
 // scene_capi.cpp — include/vct_host.h over vcthost::Model (CPU only).
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <new>
+#include <string>
 
 #include "../../include/vct_host.h"
 #include "camera.h"
@@ -14,17 +16,31 @@ struct vcth_model {
 
 extern "C" {
 
+namespace {
+void put_err(char* err, int errlen, const std::string& e) {
+    if (err && errlen > 0) {
+        std::strncpy(err, e.c_str(), (size_t)errlen - 1);
+        err[errlen - 1] = 0;
+    }
+}
+}  // namespace
+
+// No C++ exception crosses the C ABI: an allocation failure (std::bad_alloc /
+// std::length_error from a hostile file) becomes -1 with the reason in err.
 int vcth_load_obj(const char* path, vcth_model** out, char* err, int errlen) {
     if (!path || !out) return -1;
     *out = nullptr;
-    vcth_model* h = new (std::nothrow) vcth_model();
-    if (!h) return -1;
-    std::string e;
-    if (!h->m.LoadObj(path, &e)) {
-        if (err && errlen > 0) {
-            std::strncpy(err, e.c_str(), (size_t)errlen - 1);
-            err[errlen - 1] = 0;
+    vcth_model* h = nullptr;
+    try {
+        h = new vcth_model();
+        std::string e;
+        if (!h->m.LoadObj(path, &e)) {
+            put_err(err, errlen, e);
+            delete h;
+            return -1;
         }
+    } catch (const std::exception& ex) {
+        put_err(err, errlen, std::string("vcth_load_obj: ") + ex.what());
         delete h;
         return -1;
     }
@@ -92,11 +108,13 @@ int vcth_decode_png(const uint8_t* file, size_t bytes, uint8_t** data, uint32_t*
     *data = nullptr;
     vcthost::PngImage img;
     std::string e;
-    if (!vcthost::DecodePng(file, bytes, &img, &e)) {
-        if (err && errlen > 0) {
-            std::strncpy(err, e.c_str(), (size_t)errlen - 1);
-            err[errlen - 1] = 0;
+    try {
+        if (!vcthost::DecodePng(file, bytes, &img, &e)) {
+            put_err(err, errlen, e);
+            return -1;
         }
+    } catch (const std::exception& ex) {
+        put_err(err, errlen, std::string("vcth_decode_png: ") + ex.what());
         return -1;
     }
     uint8_t* out = (uint8_t*)std::malloc(img.data.size() ? img.data.size() : 1);

@@ -234,6 +234,11 @@ class Context:
         if material_map is None:
             st = self.lib.vct_voxelize_device(*args, nm)
         else:
+            # the C-ABI bounds both kd4 and the map by one n_mat: a longer map would let K1
+            # read kd4 past its end on the device (the host path checks the same)
+            if kd4 is not None and material_map.numel() != nm:
+                raise VctError(_EINVAL, f"voxelize_device: material_map has {material_map.numel()} entries for "
+                                        f"{nm} materials")
             mm = self._dev(material_map, "material_map", ("torch.int32",), max(nm, 1))
             st = self.lib.vct_voxelize_textured_device(*args, mm, material_map.numel(), uv_offset)
         self._check(st, "voxelize_device")
@@ -338,6 +343,13 @@ class Context:
 
     def comm_destroy(self):
         self._check(self.lib.vct_comm_destroy(self.h), "comm_destroy")
+
+    def comm_rank(self) -> tuple[int, int]:
+        """(rank, nranks) of the context's communicator as RCCL holds it (vct_comm_rank;
+        (0, 1) without one)."""
+        r, n = C.c_uint32(), C.c_uint32()
+        self._check(self.lib.vct_comm_rank(self.h, C.byref(r), C.byref(n)), "comm_rank")
+        return r.value, n.value
 
     def comm_set_timeout(self, timeout_ms: int):
         self._check(self.lib.vct_comm_set_timeout(self.h, int(timeout_ms)), "comm_set_timeout")

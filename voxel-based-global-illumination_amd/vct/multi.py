@@ -298,7 +298,7 @@ class FrameTracer:
         for i in range(1, self.tune_pairs):
             pairs[f"two streams ({i + 1})"] = [t.cuda.Stream(self.device) for _ in range(2)]
         pairs["two high-priority streams"] = [t.cuda.Stream(self.device, priority=-1) for _ in range(2)]
-        ms = {}
+        ms, launch = {}, {}
         for name, pair in pairs.items():
             self.drain()
             self.overlap = pair is not None
@@ -308,19 +308,26 @@ class FrameTracer:
                 self.step(gb, eye, variant=variant)
             self.drain()
             e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
+            ev = [(t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)) for _ in range(frames)]
             e0.record(main)
-            for _ in range(frames):
-                self.step(gb, eye, variant=variant)
+            for i in range(frames):
+                self.step(gb, eye, variant=variant, events=ev[i])
             self.drain()
             e1.record(main)
             e1.synchronize()
             ms[name] = e0.elapsed_time(e1) / frames
+            launch[name] = sum(a.elapsed_time(b) for a, b in ev) / frames
         best = min((k for k in pairs if pairs[k] is not None), key=lambda k: ms[k])
         self.overlap = ms[best] * gain < ms["one stream"]
         self.streams = pairs[best]
         self.tuned = {"ms": {k: round(v, 4) for k, v in ms.items()}}
         self.tuned["chosen"] = best if self.overlap else "one stream"
         self.tuned["overlap"] = self.overlap
+        # the latency paid for the throughput: a launch's start-to-end time inside each loop
+        # (overlapped, a frame's trace shares the chip with its neighbours and ends later)
+        self.tuned["launch_ms"] = {k: round(v, 4) for k, v in launch.items()}
+        ch = self.tuned["chosen"]
+        self.tuned["latency_paid_ms"] = round(launch[ch] - launch["one stream"], 4)
         return self.tuned
 
     def step(self, gb, eye, variant=0, events=None):
