@@ -471,24 +471,73 @@ def scene_arrays(name):
     return _SCENES[name]
 
 
-def relight_roofline(ctx, n, k2_ms, k3_ms):
-    """HBM fractions of the relight kernels from their algorithmic bytes:
-    K3 reads level 0 once and writes every face of levels 1..L (the block plan builds each
-    subtree in LDS; the subtree tops it reads back are < 0.1 % of that); K2 reads the
-    albedo / normal of every occupied voxel (32 B) and writes its level-0 texel (16 B);
-    its shadow walk reads the 2 MiB occupancy bitmask from L2, not counted."""
+ATOMIC_PEAK_GBS = 1300.0   # chip-wide atomic rate (MI355X_MICROARCH.md 'Global float atomics')
+RELIGHT_PROFILE = os.path.join(REPO, "profiles", "relight_counters.json")
+
+
+def load_relight_profile(n, scene):
+    """The rocprofv3 records of K1 / K2 / K3 for this grid and scene and THIS library build
+    (tools/pmc_all.sh -> profiles/relight_counters.json), or (None, reason)."""
+    try:
+        with open(RELIGHT_PROFILE) as f:
+            db = json.load(f)
+    except (OSError, ValueError) as e:
+        return None, f"no relight profile ({e.__class__.__name__})"
+    rec = db.get(f"{n}^3 {scene}")
+    if rec is None:
+        return None, f"no relight profile entry for '{n}^3 {scene}'"
+    if any(v.get("lib_sha256") != lib_sha256() for v in rec.values()):
+        return None, "relight profile measured on another library build"
+    return rec, None
+
+
+def relight_roofline(ctx, n, scene, k1_ms, k2_ms, k3_ms):
+    """Rooflines of the relight kernels.  From the rocprofv3 record of this build (per call:
+    VALU wave-instructions, HBM bytes = (2 FETCH_SIZE + WRITE_SIZE) x 1024 and, for K1, the
+    L2's atomic requests x 64 B) three rates are formed over the stage's kernel time --
+    VALU issue (1 228.8 G/s), HBM (8 TB/s), atomics (K1 only, 1.3 TB/s) -- and `bound`
+    names the most loaded.  K2 / K3 use the bench's own time (10 calls queued back to
+    back); K1's host-timed call includes a host read-back of its candidate count, so its
+    rates use the record's summed kernel durations (`kernel_ms`).  The algorithmic bytes
+     stay beside them: K3 reads level 0 once and writes every face of levels
+    1..L; K2 reads the albedo / normal of every occupied voxel (32 B) and writes its
+    level-0 texel (16 B)."""
     import numpy as np
     L = int(math.log2(n))
     k3_bytes = n ** 3 * 16 + sum(6 * (n >> l) ** 3 * 16 for l in range(1, L + 1))
     ao, _ = ctx.download_voxels()
     occ = int(np.count_nonzero(ao[..., 3] > 0))
     k2_bytes = occ * 48
+    rec, reason = load_relight_profile(n, scene)
     out = {}
-    for name, b, ms, bound in (("k3", k3_bytes, k3_ms, "hbm"), ("k2", k2_bytes, k2_ms, "shadow-walk latency")):
-        gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else None
-        out[f"{name}_roofline"] = {"bound": bound, "bytes": b, "achieved": round(gbs, 1) if gbs else None,
-                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None}
+    for name, alg, ms in (("k1", None, k1_ms), ("k2", k2_bytes, k2_ms), ("k3", k3_bytes, k3_ms)):
+        r = {"bytes": alg, "bench_ms": round(ms, 4) if ms else None}
+        if alg is not None and ms:
+            gbs = alg / (ms * 1e-3) / 1e9
+            r["algorithmic_GBs"] = round(gbs, 1)
+            r["algorithmic_frac"] = round(gbs / HBM_PEAK_GBS, 4)
+        st = (rec or {}).get(name)
+        if st is None:
+            r.update({"bound": None, "frac": None, "note": reason or f"no {name} record"})
+            out[f"{name}_roofline"] = r
+            continue
+        t_ms = st["kernel_ms_per_call"] if name == "k1" else ms
+        t = t_ms * 1e-3
+        rates = {"issue (VALU)": (st.get("SQ_INSTS_VALU", 0) / t / 1e9, VALU_PEAK_G, "G VALU wave-instr/s"),
+                 "hbm": (st.get("hbm_bytes_per_call", 0) / t / 1e9, HBM_PEAK_GBS, "GB/s")}
+        if name == "k1":
+            rates["atomics"] = (st.get("atomic_bytes_per_call", 0) / t / 1e9, ATOMIC_PEAK_GBS, "GB/s")
+        bound = max(rates, key=lambda k_: rates[k_][0] / rates[k_][1])
+        ach, peak, unit = rates[bound]
+        r.update({"bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": unit,
+                  "frac": round(ach / peak, 4), "kernel_ms": round(t_ms, 4),
+                  "rates": {k_: {"achieved": round(v[0], 1), "peak": v[1], "unit": v[2], "frac": round(v[0] / v[1], 4)}
+                            for k_, v in rates.items()},
+                  "traffic": st.get("hbm_bytes_per_call"), "l2_hit_rate": round(st.get("l2_hit_rate", 0.0), 4),
+                  "wait_any": round(st.get("wait_any", 0.0), 4), "issue_active": round(st.get("issue_active", 0.0), 4),
+                  "kernels": st.get("kernels"), "profile": f"profiles/relight_counters.json#{n}^3 {scene}",
+                  "profile_tag": st.get("tag")})
+        out[f"{name}_roofline"] = r
     out["k2_roofline"]["occupied_voxels"] = occ
     return out
 
@@ -557,7 +606,7 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     k3_ms = timed_queued(ctx.build_mips)
     r.update({"k2_inject_ms": round(k2_ms, 3), "k3_mips_ms": round(k3_ms, 3), "grid_bcast_ms": round(bcast_ms, 3)})
     if relight_roofs:
-        r.update(relight_roofline(ctx, n, k2_ms, k3_ms))
+        r.update(relight_roofline(ctx, n, scene_name, r["k1_voxelize_ms"], k2_ms, k3_ms))
 
     cam = Camera()
     eye = [float(x) for x in cam.position]
@@ -972,7 +1021,7 @@ def run(args, world):
         result["k4_form"] = form_name(m["k4_form"])
         for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
                    "frame_relight_bcast_ms", "frame_relight_replicated_ms", "replicated_k2_equals_bcast",
-                   "trace_ms_max_rank", "gather_ms", "allgather_ms", "k2_roofline", "k3_roofline"):
+                   "trace_ms_max_rank", "gather_ms", "allgather_ms", "k1_roofline", "k2_roofline", "k3_roofline"):
             if k_ in m:
                 result[k_] = m[k_]
         result["roofline"] = roof

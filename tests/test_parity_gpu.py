@@ -575,7 +575,8 @@ def test_frame_tracer_tune(gpu_ready):
     for f, e in enumerate(eyes):
         tr.step(gb, e)
         if f == 0:
-            assert not tr.auto and {"ms", "chosen", "overlap"} == set(tr.tuned)
+            assert not tr.auto and {"ms", "chosen", "overlap", "launch_ms", "latency_paid_ms"} == set(tr.tuned)
+            assert set(tr.tuned["launch_ms"]) == set(tr.tuned["ms"])
             assert len(tr.tuned["ms"]) == 2 + tr.tune_pairs and tr.tuned["chosen"] in tr.tuned["ms"]
     tr.drain()
     torch.cuda.synchronize()
