@@ -164,6 +164,49 @@ def test_trace_parity(gpu_ready, oracle_mod, name, n, kind, aniso, nd, spec):
     ctx.close()
 
 
+@pytest.mark.parametrize("n", [16, 64])
+def test_empty_space_maps_exact(gpu_ready, oracle_mod, n, monkeypatch):
+    """K4's empty-space test (Grid::zmap, rebuilt by build_mips from the level-0 texels
+    K3 reads): a sparse uploaded level 0 with signed values, -0.0, denormals and alpha-0
+    texels, traced from random surface points and normals with random roughness.  The
+    frame equals the oracle bit for bit, and equals the frame traced without the maps
+    (VCT_ZMAP=0); steps and per-pixel steps too."""
+    from vct import Context
+    rng = np.random.default_rng(17 + n)
+    occ = rng.random((n, n, n)) < 0.02
+    r0 = np.zeros((n, n, n, 4), np.float32)
+    r0[occ] = rng.standard_normal((int(occ.sum()), 4)).astype(np.float32)
+    free = np.argwhere(~occ)
+    pick = free[rng.choice(len(free), 60, replace=False)]
+    r0[tuple(pick[:20].T)] = -0.0                                   # negative zero: not +0
+    r0[tuple(pick[20:40].T)] = np.float32(1e-40)                    # denormal
+    r0[tuple(pick[40:].T)] = np.array([0.5, -0.25, 0.125, 0.0], np.float32)   # colour with alpha 0
+    w, h = 96, 64
+    pos = np.zeros((h, w, 4), np.float32)
+    pos[..., :3] = rng.uniform(0.05, 0.95, (h, w, 3))
+    pos[..., 3] = (rng.random((h, w)) < 0.9).astype(np.float32)
+    nv = rng.standard_normal((h, w, 3))
+    nrm = np.zeros((h, w, 4), np.float32)
+    nrm[..., :3] = nv / np.linalg.norm(nv, axis=-1, keepdims=True)
+    alb = np.zeros((h, w, 4), np.float32)
+    alb[..., :3] = rng.random((h, w, 3))
+    alb[..., 3] = rng.uniform(0.0, 1.0, (h, w))
+    eye = (0.5, 0.6, 2.5)
+    ctx = Context(n, (0, 0, 0), 1.0)
+    ctx.upload_level0(r0)
+    ctx.build_mips()
+    got = ctx.trace(pos, nrm, alb, eye)
+    ref = oracle_mod.trace(n, (0, 0, 0), 1.0, r0, gpu_pyramid_flat(ctx), pos, nrm, alb, eye)
+    for key in ("diffuse", "spec", "steps_px"):
+        assert np.array_equal(got[key], ref[key]), key
+    monkeypatch.setenv("VCT_ZMAP", "0")
+    ctx.build_mips()
+    off = ctx.trace(pos, nrm, alb, eye)
+    for key in ("diffuse", "spec", "steps_px"):
+        assert np.array_equal(got[key], off[key]), key
+    ctx.close()
+
+
 @pytest.mark.parametrize("kind", ["scene", "jitter"])
 def test_occupancy_form_curved_bitexact(gpu_ready, oracle_mod, kind):
     """Curved surfaces in the occupancy form: cones whose valid lanes select four faces

@@ -194,6 +194,24 @@ vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
     if (e == hipSuccess) e = hipMemset(g.albedo_occ, 0, nv * sizeof(float4));
     if (e == hipSuccess) e = hipMemset(g.normal, 0, nv * sizeof(float4));
     if (e == hipSuccess) e = hipMemset(g.occ_bits, 0, (nv / 64) * 8);
+    if (e == hipSuccess && g.n >= 16) {
+        // K4 empty-space maps (Grid::zmap): level-0 bits, occupancy bytes of levels 2.., bit maps
+        // every map level keeps >= 4 texels per axis (its rows are read as dwords)
+        g.zm_levels = (int)(g.L - 2 < (uint32_t)Grid::kZLevels ? g.L - 2 : (uint32_t)Grid::kZLevels);
+        uint64_t ob = 0;
+        uint32_t zw = 0;
+        for (int m = 1; m <= g.zm_levels; ++m) {
+            const uint64_t nm = g.n >> m;
+            if (m >= 2) { g.occ_off[m] = ob; ob += nm * nm * nm; }
+            g.zm_dim[m] = (uint32_t)nm + 1u;
+            g.zm_rw[m] = (g.zm_dim[m] + 31u) / 32u;
+            g.zm_off[m] = zw;
+            zw += g.zm_dim[m] * g.zm_dim[m] * g.zm_rw[m];
+        }
+        e = hipMalloc((void**)&g.b0, nv / 8);
+        if (e == hipSuccess) e = hipMalloc((void**)&g.occ, ob ? ob : 1);
+        if (e == hipSuccess) e = hipMalloc((void**)&g.zmap, (size_t)zw * 4);
+    }
     if (e == hipSuccess) e = hipMalloc((void**)&g.occ_list, nv * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&g.occ_count, 256);
     if (e == hipSuccess) e = hipMemset(g.occ_count, 0, 256);
@@ -274,6 +292,9 @@ void vct_destroy(vct_ctx* c) {
     if (g.normal) (void)hipFree(g.normal);
     if (g.occ_bits) (void)hipFree(g.occ_bits);
     if (g.occ_list) (void)hipFree(g.occ_list);
+    if (g.b0) (void)hipFree(g.b0);
+    if (g.occ) (void)hipFree(g.occ);
+    if (g.zmap) (void)hipFree(g.zmap);
     if (g.occ_count) (void)hipFree(g.occ_count);
     if (g.accum) (void)hipFree(g.accum);
     if (c->k1_err) (void)hipFree(c->k1_err);

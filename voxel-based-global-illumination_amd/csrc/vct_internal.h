@@ -30,6 +30,24 @@ struct Grid {
     unsigned long long* occ_bits = nullptr;  // [n^3 / 64] occupancy bitmask
     uint32_t* occ_list = nullptr;            // [n^3] the occupied voxels of the last K1 (k2_list order)
     uint32_t* occ_count = nullptr;           // [1] entries of occ_list
+    // K4 empty-space maps (vct_mips.hip, rebuilt by every build_mips): b0 = one bit per
+    // level-0 texel, set iff the texel is not +0 (bit order = the texel's index in the brick
+    // layout, so byte v = the eight children of level-1 texel v); occ = per level m >= 2 one
+    // byte per texel, nonzero iff some level-0 texel under it is; zmap = per level m = 1..zm_levels
+    // one bit per position p in [-1, n_m - 1]^3 (stored at p + 1), set iff any level-m texel of
+    // p + {0,1}^3 may be nonzero.  A level-l trilinear footprint at corner c lies under the
+    // level-(l+1) texels c >> 1 + {0,1}^3, so a clear bit of map l+1 at c >> 1 proves the
+    // footprint's texels (every face) are +0.
+    static constexpr int kZLevels = 5;
+    uint32_t* b0 = nullptr;                  // [n^3 / 32]
+    uint8_t* occ = nullptr;                  // levels 2..zm_levels, byte per texel, back to back
+    uint64_t occ_off[kZLevels + 1] = {};     // byte offset of level m in occ (m >= 2)
+    uint32_t* zmap = nullptr;                // maps 1..zm_levels, back to back
+    uint32_t zm_off[kZLevels + 1] = {};      // dword offset of map m
+    uint32_t zm_dim[kZLevels + 1] = {};      // n_m + 1 positions per axis
+    uint32_t zm_rw[kZLevels + 1] = {};       // dwords per row of map m
+    int zm_levels = 0;
+    bool zm_valid = false;                   // the maps describe the current pyramid
     bool voxelized = false, injected = false, mipped = false;
     bool l0_dense = false;   // level 0 was replaced densely (upload / device copy): K2 must clear it whole
     bool l0_on_peers = false;   // multi-device: the other devices hold this level 0 (vct_build_mips copies it)
@@ -186,7 +204,7 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts,
                            uint32_t uv_offset, int* d_err);
 // K2
 hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb);
-// K3
+// K3 (and the K4 empty-space maps of Grid::zmap)
 hipError_t launch_mips(vct_ctx* c);
 // one nl^3 face volume between the pyramid's texel layout and linear-Z (vct_device.h)
 hipError_t launch_relayout(vct_ctx* c, const float4* src, float4* dst, uint32_t nl, bool to_linear);

@@ -195,6 +195,7 @@ struct BlockK {
     uint64_t off[kMaxLevels + 1];             // float4 offset of each level
     int n, l;                                 // grid edge, first level built
     int brick_writes;                         // level l stored in brick order from LDS (VCT_K3_WRITE)
+    uint32_t* b0;                             // level 1 from level 0: the level-0 nonzero bits (Grid::b0), or null
 };
 
 template <int MODE, int BZ>
@@ -229,6 +230,21 @@ __global__ void __launch_bounds__(kBlk * kBlk * BZ) k3_block(const BlockK k) {
         for (int i = 0; i < 8; ++i) {
             const int u = i * kT + t;
             if (u <= lim) st[(u >> 3) * 9 + (u & 7)] = r[i];
+        }
+        if (MODE != kFace && k.b0 && E == kBlk) {
+            // the K4 empty-space maps' input: a wave's load i covers the eight child bricks of
+            // one x-row of parents, 64 consecutive level-0 texel indices starting at a
+            // multiple of 64, so its ballot of "not +0" is one 64-bit word of Grid::b0
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const unsigned long long m = __builtin_amdgcn_ballot_w64(
+                    (__float_as_uint(r[i].x) | __float_as_uint(r[i].y) | __float_as_uint(r[i].z) |
+                     __float_as_uint(r[i].w)) != 0u);
+                const int c = (i * kT + (t & ~63)) >> 3;
+                const uint32_t cy = (uint32_t)((c / E) % E), cz = (uint32_t)(c / (E * E));
+                const size_t brick = (size_t)X0 + (size_t)nl * ((size_t)(Y0 + cy) + (size_t)nl * (Z0 + cz));
+                if ((t & 63) == 0) reinterpret_cast<unsigned long long*>(k.b0)[brick >> 3] = m;
+            }
         }
     }
     __syncthreads();
@@ -302,6 +318,81 @@ __global__ void __launch_bounds__(kBlk * kBlk * BZ) k3_block(const BlockK k) {
     }
 }
 
+// K4 empty-space maps (Grid::zmap).  occ(m, v): level-m texel v (linear-Z) may be nonzero.
+// m = 1 reads the byte of b0 holding the eight level-0 children of v (brick order); m >= 2
+// reads the occupancy bytes built from the level below.
+__device__ __forceinline__ bool occ_at_level(const uint8_t* __restrict__ b0, const uint8_t* __restrict__ occ,
+                                             uint32_t nm, uint32_t x, uint32_t y, uint32_t z) {
+    const size_t v = (size_t)x + (size_t)nm * ((size_t)y + (size_t)nm * z);
+    return (b0 ? b0[v] : occ[v]) != 0;
+}
+
+// level-m occupancy bytes from level m-1 (m = 2: from b0)
+__global__ void __launch_bounds__(256) k_occ_down(const uint8_t* __restrict__ b0, const uint8_t* __restrict__ src,
+                                                  uint8_t* __restrict__ dst, uint32_t nm) {
+    const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= (size_t)nm * nm * nm) return;
+    const uint32_t x = (uint32_t)(v % nm), y = (uint32_t)((v / nm) % nm), z = (uint32_t)(v / ((size_t)nm * nm));
+    const uint32_t ns = 2u * nm;
+    bool any = false;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+        any |= occ_at_level(b0, src, ns, 2u * x + (a & 1), 2u * y + ((a >> 1) & 1), 2u * z + (a >> 2));
+    dst[v] = any ? 1u : 0u;
+}
+
+// map m: bit of padded position P (p = P - 1 in [-1, nm - 1]^3) = OR of occ over p + {0,1}^3.
+// One thread per dword (32 positions of a row): per texel row (y, z) it packs the
+// occupancy of texels x0 - 1 .. x0 + 31 (x0 = 32 wx) from nine dword loads of the byte map,
+// dilates along x (bit b | bit b + 1) and ORs the four rows p_y + {0,1} x p_z + {0,1}.
+__global__ void __launch_bounds__(256) k_zbits(const uint8_t* __restrict__ bytes, uint32_t nm,
+                                               uint32_t* __restrict__ dst, uint32_t dim, uint32_t rw) {
+    const size_t wi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (wi >= (size_t)dim * dim * rw) return;
+    const uint32_t wx = (uint32_t)(wi % rw), py = (uint32_t)((wi / rw) % dim), pz = (uint32_t)(wi / ((size_t)rw * dim));
+    const int x0 = (int)(wx * 32u);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int y = (int)py - 1 + (r & 1), z = (int)pz - 1 + (r >> 1);
+        if (y < 0 || z < 0 || y >= (int)nm || z >= (int)nm) continue;
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(bytes + ((size_t)z * nm + (size_t)y) * nm);
+        unsigned long long t = 0;                    // bit b: texel x0 - 1 + b may be nonzero
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            const int o = x0 - 4 + 4 * q;            // texels o .. o + 3 (nm is a multiple of 4)
+            if (o < 0 || o >= (int)nm) continue;
+            const uint32_t v = row[o >> 2];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int b = o + j - x0 + 1;        // texels x0 - 4 .. x0 - 2 fall outside
+                if (b >= 0 && ((v >> (8 * j)) & 0xffu)) t |= 1ull << b;
+            }
+        }
+        bits |= (uint32_t)(t | (t >> 1));
+    }
+    dst[wi] = bits;
+}
+
+hipError_t launch_zmaps(vct_ctx* c) {
+    Grid& g = c->grid;
+    for (int m = 2; m <= g.zm_levels; ++m) {
+        const uint32_t nm = g.n >> m;
+        const size_t cnt = (size_t)nm * nm * nm;
+        hipLaunchKernelGGL(k_occ_down, dim3((uint32_t)((cnt + 255) / 256)), dim3(256), 0, c->stream,
+                           m == 2 ? (const uint8_t*)g.b0 : nullptr, m == 2 ? nullptr : g.occ + g.occ_off[m - 1],
+                           g.occ + g.occ_off[m], nm);
+    }
+    for (int m = 1; m <= g.zm_levels; ++m) {
+        // level 1's occupancy bytes are b0 itself (byte v = the children of texel v)
+        const size_t words = (size_t)g.zm_dim[m] * g.zm_dim[m] * g.zm_rw[m];
+        hipLaunchKernelGGL(k_zbits, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, c->stream,
+                           m == 1 ? (const uint8_t*)g.b0 : g.occ + g.occ_off[m], g.n >> m, g.zmap + g.zm_off[m],
+                           g.zm_dim[m], g.zm_rw[m]);
+    }
+    return hipGetLastError();
+}
+
 // one face volume between the pyramid's layout and linear-Z (download / upload)
 __global__ void __launch_bounds__(256) k_relayout(const float4* __restrict__ src, float4* __restrict__ dst, uint32_t nl,
                                                   int to_linear) {
@@ -318,8 +409,9 @@ __global__ void __launch_bounds__(256) k_relayout(const float4* __restrict__ src
 
 hipError_t launch_mips(vct_ctx* c) {
     Grid& g = c->grid;
+    g.zm_valid = false;
     const char* plan = getenv("VCT_K3_PLAN");
-    if (plan && strcmp(plan, "level") == 0) {    // A/B: one lane-per-parent launch per level
+    if (plan && strcmp(plan, "level") == 0) {    // A/B: one lane-per-parent launch per level (no K4 maps)
         for (uint32_t l = 1; l <= g.L; ++l) {
             const int nl = (int)(g.n >> l);
             const size_t vl = (size_t)nl * nl * nl;
@@ -345,6 +437,7 @@ hipError_t launch_mips(vct_ctx* c) {
         return v ? atoi(v) : 1;
     }();
     k.brick_writes = bw;
+    k.b0 = nullptr;
     // block depth: 8 x 8 x 4 parents (256 threads, 36 KB of LDS, subtrees three levels
     // deep) beat the 8^3 cube (512 threads, 72 KB, four levels) by 4 % at 256^3 and 9 % at
     // 512^3, and 8 x 8 x 2 by 3-4 %: twice the workgroups in flight per CU hide the staging
@@ -360,6 +453,7 @@ hipError_t launch_mips(vct_ctx* c) {
         const uint32_t nbk = nl / E, all = nbk * nbk * (nl / Ez);
         const uint32_t blocks = all;
         k.l = (int)l;
+        k.b0 = (l == 1 && g.zm_levels > 0) ? g.b0 : nullptr;   // the launch that reads level 0
 #define VCT_K3_LAUNCH(BZv)                                                                                      \
     do {                                                                                                        \
         constexpr uint32_t thr = (uint32_t)(kBlk * kBlk * BZv);                                                \
@@ -372,6 +466,11 @@ hipError_t launch_mips(vct_ctx* c) {
         else VCT_K3_LAUNCH(4);
 #undef VCT_K3_LAUNCH
         l += (uint32_t)__builtin_ctz(Ez) + 1u;
+    }
+    if (g.zm_levels > 0) {
+        hipError_t e = launch_zmaps(c);
+        if (e != hipSuccess) return e;
+        g.zm_valid = !(getenv("VCT_ZMAP") && strcmp(getenv("VCT_ZMAP"), "0") == 0);   // VCT_ZMAP=0: A/B without
     }
     return hipGetLastError();
 }
