@@ -109,7 +109,7 @@ __device__ __forceinline__ float lvl_coord(float q, float scale) {
 
 // the occupancy form of the default cone trace: 96 VGPRs, 7008 B of LDS (no four-face
 // union), 5 waves/SIMD; the union form runs kUnionWaves (K4Tuner picks per workload)
-constexpr int kOccWaves = 5;
+constexpr int kOccWaves = 5;   // 6 (80 VGPRs) spills 54-69 VGPRs
 constexpr int kUnionWaves = 4;  // __launch_bounds__ minimum waves per SIMD (128 VGPRs, 9344 B of LDS)
 
 namespace vct {
@@ -788,9 +788,27 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // only (+3 %), only on level A's gather path (+1 %), only for levels <= 1 or <= 2 (the
     // gain shrinks), maps up to level 5 instead of 4 (+0.5 %), and the bit of the next
     // step's level A loaded one step ahead (its position and corner VALU: +7 %).
+    // level B restages first: its loads go out before level A's empty-space test waits, so
+    // the two round trips overlap (A/B: atrium -1.0 %, courtyard -0.3 %)
+    bool stB = false;
+    if (needB && !useB && (modeB != kFaces || faces_okB)) {
+        BrickEntry nb{};
+        nb.lvl = l1;
+        if (brick_origin(cB, amB, cc.neg, nb, z3B)) {
+            bB = nb;
+            bc.b = nb;
+            useB = stB = true;
+        }
+    }
+    Tex4 tB;
+    if (stB) tB = stage_load<O32, AM>(k, l1, bB, modeB, cc);
     const unsigned long long nzA = useA ? amA : wballot(zbit(k, l0, cA) != 0u) & amA;
     const bool emptyA = nzA == 0ull;                  // the sample is exactly +0
     if (!useA && emptyA) VCT_DBG(32);
+    // a brick whose texels are all +0 (empty space) is marked: its samples are exactly
+    // zero (fmaf(w, +0, +0) = +0 through the whole trilinear chain), so hits on it skip
+    // the LDS reads and the FMAs
+    if (stB) bB.zero = bc.b.zero = wall(stage_store<AM>(modeB, cc, tB, ldsB));
     bool stA = false;
     if (!useA && !emptyA && (modeA != kFaces || faces_okA)) {
         BrickEntry nb{};
@@ -801,41 +819,13 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
             useA = stA = true;
         }
     }
-    bool stB = false;
-    if (needB) {
-        if (!useB && (modeB != kFaces || faces_okB)) {
-            BrickEntry nb{};
-            nb.lvl = l1;
-            if (brick_origin(cB, amB, cc.neg, nb, z3B)) {
-                bB = nb;
-                bc.b = nb;
-                useB = stB = true;
-            }
-        }
-    }
     VCT_DBG(useA ? (stA ? 2 : 3) : 1);
     VCT_DBG(needB ? (useB ? (stB ? 27 : 26) : 28) : 31);   // level B: hit / staged / gathered / not sampled
     if (useA && modeA == kFaces) VCT_DBG(29);               // brick samples read three faces per corner
     if (useB && modeB == kFaces) VCT_DBG(30);
     pc.mark(1);
-    // a brick whose texels are all +0 (empty space) is marked: its samples are exactly
-    // zero (fmaf(w, +0, +0) = +0 through the whole trilinear chain), so hits on it skip
-    // the LDS reads and the FMAs
-    if (stA && stB) {
-        const Tex4 tA = stage_load<O32, AM>(k, l0, bA, modeA, cc);
-        const Tex4 tB = stage_load<O32, AM>(k, l1, bB, modeB, cc);
-        const bool zA = stage_store<AM>(modeA, cc, tA, ldsA);
-        const bool zB = stage_store<AM>(modeB, cc, tB, ldsB);
-        bA.zero = bc.a.zero = wall(zA);
-        bB.zero = bc.b.zero = wall(zB);
-        wave_lds_sync();
-    } else if (stA) {      // one level restages: a staging copy per level (no selects between the two)
-        bA.zero = bc.a.zero = wall(stage_store<AM>(modeA, cc, stage_load<O32, AM>(k, l0, bA, modeA, cc), ldsA));
-        wave_lds_sync();
-    } else if (stB) {
-        bB.zero = bc.b.zero = wall(stage_store<AM>(modeB, cc, stage_load<O32, AM>(k, l1, bB, modeB, cc), ldsB));
-        wave_lds_sync();
-    }
+    if (stA) bA.zero = bc.a.zero = wall(stage_store<AM>(modeA, cc, stage_load<O32, AM>(k, l0, bA, modeA, cc), ldsA));
+    if (stA || stB) wave_lds_sync();
     pc.mark(2);
     float4 sA = z4, sB = z4;
     const bool readA = useA && !bA.zero, readB = useB && !bB.zero;
