@@ -345,11 +345,8 @@ __global__ void __launch_bounds__(256) k_occ_down(const uint8_t* __restrict__ b0
 // One thread per dword (32 positions of a row): per texel row (y, z) it packs the
 // occupancy of texels x0 - 1 .. x0 + 31 (x0 = 32 wx) from nine dword loads of the byte map,
 // dilates along x (bit b | bit b + 1) and ORs the four rows p_y + {0,1} x p_z + {0,1}.
-__global__ void __launch_bounds__(256) k_zbits(const uint8_t* __restrict__ bytes, uint32_t nm,
-                                               uint32_t* __restrict__ dst, uint32_t dim, uint32_t rw) {
-    const size_t wi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (wi >= (size_t)dim * dim * rw) return;
-    const uint32_t wx = (uint32_t)(wi % rw), py = (uint32_t)((wi / rw) % dim), pz = (uint32_t)(wi / ((size_t)rw * dim));
+__device__ __forceinline__ uint32_t zbits_word(const uint8_t* __restrict__ bytes, uint32_t nm, uint32_t wx,
+                                               uint32_t py, uint32_t pz) {
     const int x0 = (int)(wx * 32u);
     uint32_t bits = 0;
 #pragma unroll
@@ -371,22 +368,119 @@ __global__ void __launch_bounds__(256) k_zbits(const uint8_t* __restrict__ bytes
         }
         bits |= (uint32_t)(t | (t >> 1));
     }
-    dst[wi] = bits;
+    return bits;
 }
 
-hipError_t launch_zmaps(vct_ctx* c) {
+__global__ void __launch_bounds__(256) k_zbits(const uint8_t* __restrict__ bytes, uint32_t nm,
+                                               uint32_t* __restrict__ dst, uint32_t dim, uint32_t rw) {
+    const size_t wi = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (wi >= (size_t)dim * dim * rw) return;
+    dst[wi] = zbits_word(bytes, nm, (uint32_t)(wi % rw), (uint32_t)((wi / rw) % dim), (uint32_t)(wi / ((size_t)rw * dim)));
+}
+
+struct OccOffsets {
+    uint64_t off[Grid::kZLevels + 1];
+};
+struct ZMapsK {
+    int levels;
+    uint32_t end[Grid::kZLevels + 1];       // exclusive end dword of map m (maps back to back)
+    uint32_t dim[Grid::kZLevels + 1], rw[Grid::kZLevels + 1], occ_off[Grid::kZLevels + 1];
+};
+
+// Occupancy bytes of levels 2 .. 5 in one launch: a 256-thread workgroup owns a 16^3
+// block of level-1 texels (one 16-byte row segment of b0's bytes per thread), reduces it to
+// 8^3 / 4^3 / 2^3 / 1 texels of levels 2 / 3 / 4 / 5 through LDS bit rows and writes
+// those levels' bytes (levels above `top` are skipped).  Needs n_1 >= 16.
+__global__ void __launch_bounds__(256) k_occ_pyr(const uint8_t* __restrict__ b0, uint8_t* __restrict__ occ,
+                                                 OccOffsets o, uint32_t n1, int top) {
+    __shared__ uint32_t rows[256];                 // bit rows of the current level, [z][y]
+    const uint32_t t = threadIdx.x;
+    const uint32_t nb = n1 / 16u, b = blockIdx.x;
+    const uint32_t X0 = (b % nb) * 16u, Y0 = ((b / nb) % nb) * 16u, Z0 = (b / (nb * nb)) * 16u;
+    {
+        const uint32_t y = t & 15u, z = t >> 4;
+        const uint4 v = *reinterpret_cast<const uint4*>(b0 + ((size_t)(Z0 + z) * n1 + (Y0 + y)) * n1 + X0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t m = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m |= ((w[i >> 2] >> (8 * (i & 3))) & 0xffu) ? 1u << i : 0u;
+        rows[t] = m;
+    }
+    __syncthreads();
+    // level m (edge e = 16 >> (m - 1) texels of the block): row (y, z) = OR of the four
+    // level-(m-1) rows (2y .. 2y+1, 2z .. 2z+1), x pairs merged
+    uint32_t e_in = 16u;
+    for (int m = 2; m <= 5; ++m) {
+        const uint32_t e = e_in >> 1;
+        uint32_t r = 0;
+        const bool mine = t < e * e;
+        if (mine) {
+            const uint32_t y = t % e, z = t / e;
+            const uint32_t in = rows[(2u * z) * e_in + 2u * y] | rows[(2u * z) * e_in + 2u * y + 1u] |
+                                rows[(2u * z + 1u) * e_in + 2u * y] | rows[(2u * z + 1u) * e_in + 2u * y + 1u];
+            for (uint32_t x = 0; x < e; ++x) r |= ((in >> (2u * x)) & 3u) ? 1u << x : 0u;
+            if (m <= top) {
+                const uint32_t nm = n1 >> (m - 1);
+                uint8_t* dst = occ + o.off[m] + ((size_t)((Z0 >> (m - 1)) + z) * nm + ((Y0 >> (m - 1)) + y)) * nm +
+                               (X0 >> (m - 1));
+                for (uint32_t x = 0; x < e; ++x) dst[x] = (uint8_t)((r >> x) & 1u);
+            }
+        }
+        __syncthreads();
+        if (mine) rows[t] = r;
+        __syncthreads();
+        e_in = e;
+    }
+}
+
+// every map's dwords in one launch (k_zbits per dword, the map found from the offsets)
+__global__ void __launch_bounds__(256) k_zbits_all(const uint8_t* __restrict__ b0, const uint8_t* __restrict__ occ,
+                                                   ZMapsK z, uint32_t* __restrict__ dst) {
+    const uint32_t wi = blockIdx.x * blockDim.x + threadIdx.x;
+    int m = 1;
+    while (m < z.levels && wi >= z.end[m]) ++m;
+    if (wi >= z.end[m]) return;
+    const uint32_t first = m == 1 ? 0u : z.end[m - 1];
+    const uint8_t* bytes = m == 1 ? b0 : occ + z.occ_off[m];
+    const uint32_t dim = z.dim[m], rw = z.rw[m], nm = dim - 1u, li = wi - first;
+    const uint32_t wx = li % rw, py = (li / rw) % dim, pz = li / (rw * dim);
+    dst[wi] = zbits_word(bytes, nm, wx, py, pz);
+}
+
+hipError_t launch_zmaps(vct_ctx* c, hipStream_t st) {
     Grid& g = c->grid;
+    const uint32_t n1 = g.n >> 1;
+    if (n1 >= 16) {
+        OccOffsets o{};
+        for (int m = 2; m <= Grid::kZLevels; ++m) o.off[m] = g.occ_off[m];
+        const uint32_t nb = n1 / 16u;
+        hipLaunchKernelGGL(k_occ_pyr, dim3(nb * nb * nb), dim3(256), 0, st, (const uint8_t*)g.b0, g.occ, o, n1,
+                           g.zm_levels);
+        ZMapsK z{};
+        z.levels = g.zm_levels;
+        uint32_t end = 0;
+        for (int m = 1; m <= g.zm_levels; ++m) {
+            end += g.zm_dim[m] * g.zm_dim[m] * g.zm_rw[m];
+            z.end[m] = end;
+            z.dim[m] = g.zm_dim[m];
+            z.rw[m] = g.zm_rw[m];
+            z.occ_off[m] = (uint32_t)g.occ_off[m];
+        }
+        hipLaunchKernelGGL(k_zbits_all, dim3((end + 255) / 256), dim3(256), 0, st, (const uint8_t*)g.b0,
+                           (const uint8_t*)g.occ, z, g.zmap);
+        return hipGetLastError();
+    }
     for (int m = 2; m <= g.zm_levels; ++m) {
         const uint32_t nm = g.n >> m;
         const size_t cnt = (size_t)nm * nm * nm;
-        hipLaunchKernelGGL(k_occ_down, dim3((uint32_t)((cnt + 255) / 256)), dim3(256), 0, c->stream,
+        hipLaunchKernelGGL(k_occ_down, dim3((uint32_t)((cnt + 255) / 256)), dim3(256), 0, st,
                            m == 2 ? (const uint8_t*)g.b0 : nullptr, m == 2 ? nullptr : g.occ + g.occ_off[m - 1],
                            g.occ + g.occ_off[m], nm);
     }
     for (int m = 1; m <= g.zm_levels; ++m) {
         // level 1's occupancy bytes are b0 itself (byte v = the children of texel v)
         const size_t words = (size_t)g.zm_dim[m] * g.zm_dim[m] * g.zm_rw[m];
-        hipLaunchKernelGGL(k_zbits, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, c->stream,
+        hipLaunchKernelGGL(k_zbits, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, st,
                            m == 1 ? (const uint8_t*)g.b0 : g.occ + g.occ_off[m], g.n >> m, g.zmap + g.zm_off[m],
                            g.zm_dim[m], g.zm_rw[m]);
     }
@@ -447,6 +541,7 @@ hipError_t launch_mips(vct_ctx* c) {
         const int b = v ? atoi(v) : 4;
         return b == 8 || b == 2 ? b : 4;
     }();
+    bool built = false;
     for (uint32_t l = 1; l <= g.L;) {
         const uint32_t nl = g.n >> l, E = nl < (uint32_t)kBlk ? nl : (uint32_t)kBlk;
         const uint32_t Ez = nl < (uint32_t)bz ? nl : (uint32_t)bz;
@@ -465,11 +560,16 @@ hipError_t launch_mips(vct_ctx* c) {
         else if (bz == 2) VCT_K3_LAUNCH(2);
         else VCT_K3_LAUNCH(4);
 #undef VCT_K3_LAUNCH
+        if (k.b0 && !built) {
+            // level 0's bits are written: the K4 maps (in order on the ctx stream; forked onto a
+            // side stream beside K3's top levels it measured slower at 256^3, 0.130 -> 0.139 ms)
+            const hipError_t e = launch_zmaps(c, c->stream);
+            if (e != hipSuccess) return e;
+            built = true;
+        }
         l += (uint32_t)__builtin_ctz(Ez) + 1u;
     }
-    if (g.zm_levels > 0) {
-        hipError_t e = launch_zmaps(c);
-        if (e != hipSuccess) return e;
+    if (built) {
         g.zm_valid = !(getenv("VCT_ZMAP") && strcmp(getenv("VCT_ZMAP"), "0") == 0);   // VCT_ZMAP=0: A/B without
     }
     return hipGetLastError();
