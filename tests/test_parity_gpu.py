@@ -35,6 +35,66 @@ def test_voxelize_inject_mips_bitexact(gpu_ready, oracle_mod, name, n):
     ctx.close()
 
 
+@pytest.mark.parametrize("case", ["dense_voxel", "large_kd"])
+def test_voxelize_packed_sums_fallback(gpu_ready, oracle_mod, case):
+    """K1's packed accumulators (two 16.16 sums per 64-bit atomic) are exact while a voxel's
+    count x max|value| < 2^31.  dense_voxel: 40 000 small triangles in one voxel (count
+    40 000 x 65 536 > 2^31) -- the packed pass flags the overflow and K1 repeats unpacked;
+    large_kd: Kd = 300 (max|value| ~ 2^24.2) -- too few hits fit, K1 goes unpacked at once.
+    Sums, counts and voxels equal the oracle's either way, and a normal scene afterwards
+    packs again."""
+    from vct import Context
+    n = 8
+    rng = np.random.default_rng(11)
+    T = 40000 if case == "dense_voxel" else 64
+    c = np.array([4.5, 4.5, 4.5], np.float32) / n           # one voxel's centre (unit box)
+    v = (c + rng.uniform(-0.3, 0.3, (T, 3, 3)).astype(np.float32) / n).reshape(-1, 3)
+    if case == "large_kd":
+        v = rng.uniform(0.05, 0.95, (T * 3, 3)).astype(np.float32)
+    idx = np.arange(3 * T, dtype=np.uint32)
+    mat = (np.arange(T) % 2).astype(np.uint32)
+    kd = np.array([[0.9, 0.2, 1.0, 1.0], [0.3, 1.0, 0.1, 1.0]], np.float32)
+    if case == "large_kd":
+        kd = kd * 300.0
+    ctx = Context(n, (0.0, 0.0, 0.0), 1.0)
+    for _ in range(2):
+        ctx.voxelize(v, idx, mat, kd)
+        ref_s, ref_c = oracle_mod.voxelize(n, (0.0, 0.0, 0.0), 1.0, v, idx, mat, kd)
+        sums, counts = ctx.download_accum()
+        assert np.array_equal(counts, ref_c) and np.array_equal(sums, ref_s)
+        if case == "dense_voxel":
+            assert counts.max() > 32768
+        ref = oracle_mod.resolve(n, ref_s, ref_c)
+        ao, nm = ctx.download_voxels()
+        assert np.array_equal(ao, ref[0]) and np.array_equal(nm, ref[1])
+    # a normal scene after the fallback: packed again, still exact
+    s, (v2, i2, m2, k2) = scene_arrays("cornell")
+    from vct import scenes
+    g0, E = scenes.grid_for_unit_box(n)
+    ctx2 = Context(n, g0, E)
+    ctx2.voxelize(v2, i2, m2, k2)
+    ref_s, ref_c = oracle_mod.voxelize(n, g0, E, v2, i2, m2, k2)
+    sums, counts = ctx2.download_accum()
+    assert np.array_equal(counts, ref_c) and np.array_equal(sums, ref_s)
+    ctx.close()
+    ctx2.close()
+
+
+@pytest.mark.parametrize("name,n", [("atrium", 128), ("atrium", 256), ("courtyard", 256)])
+def test_inject_bitexact_coarse_bricks(gpu_ready, oracle_mod, name, n):
+    """K2 where the shadow walk's coarse bricks hold 2^3 / 4^3 voxels (n = 128 / 256; the
+    sizes above use one voxel per brick): level 0 equals the oracle's inject of the GPU's
+    own voxels bit for bit, for the scene light and for a light with a zero component."""
+    from vct import scenes
+    ctx, s, _, _ = gpu_pipeline(n, name)
+    ao, nm = ctx.download_voxels()
+    for light in (scenes.LIGHT_DIR, (0.0, 1.0, -0.35)):
+        ctx.inject_directional(light, scenes.LIGHT_COLOR)
+        ref = oracle_mod.inject(n, ao, nm, light, scenes.LIGHT_COLOR)
+        assert np.array_equal(ctx.download_level(0), ref), f"K2 radiance differs (light {light})"
+    ctx.close()
+
+
 @pytest.mark.parametrize("aniso", [True, False])
 @pytest.mark.parametrize("n", [4, 8, 32, 64, 128])
 def test_mips_bitexact_random_level0(gpu_ready, oracle_mod, aniso, n):

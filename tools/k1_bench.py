@@ -41,8 +41,15 @@ def main():
             torch.cuda.synchronize()
             if r:
                 ts[key].append((time.perf_counter() - t) * 1e3)
-    print(json.dumps({"scene": a.scene, "n": a.n, "tris": int(s.n_tri),
-                      **{k2: round(sorted(x)[len(x) // 2], 3) for k2, x in ts.items()}}))
+    import hashlib
+    ao, nm = ctx.download_voxels()
+    hs = hashlib.sha256(ao.tobytes() + nm.tobytes() + ctx.download_level(0).tobytes())
+    if a.n <= 256:                     # the raw accumulators too (8.6 GB of records at 512^3)
+        sums, counts = ctx.download_accum()
+        hs.update(sums.tobytes() + counts.tobytes())
+    h = hs.hexdigest()[:16]
+    print(json.dumps({"scene": a.scene, "n": a.n, "tris": int(s.n_tri), "lib": os.path.basename(os.environ.get("VCT_LIB", "")),
+                      **{k2: round(sorted(x)[len(x) // 2], 3) for k2, x in ts.items()}, "hash": h}))
 
 
 if __name__ == "__main__":

@@ -935,10 +935,21 @@ vct_status vct_download_accum(vct_ctx* c, int64_t* sums6, uint32_t* counts) {
     hipError_t e = hipMemcpyAsync(tmp, c->grid.accum, nv * 64, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) { delete[] tmp; return hip_fail(c, e, "download accum"); }
+    const bool packed = c->grid.accum_packed;
     for (size_t v = 0; v < nv; ++v) {
-        if (sums6)
-            for (int k = 0; k < 6; ++k) sums6[6 * v + k] = tmp[8 * v + k];
-        if (counts) counts[v] = (uint32_t)tmp[8 * v + 6];
+        const long long* r = tmp + 8 * v;
+        if (sums6) {
+            if (packed) {   // r + 2^32 g, b + 2^32 nx, ny + 2^32 nz (launch_voxelize)
+                for (int k = 0; k < 3; ++k) {
+                    const long long lo = (long long)(int32_t)(uint32_t)(unsigned long long)r[k];
+                    sums6[6 * v + 2 * k] = lo;
+                    sums6[6 * v + 2 * k + 1] = (long long)((unsigned long long)r[k] - (unsigned long long)lo) >> 32;
+                }
+            } else {
+                for (int k = 0; k < 6; ++k) sums6[6 * v + k] = r[k];
+            }
+        }
+        if (counts) counts[v] = (uint32_t)r[packed ? 3 : 6];
     }
     delete[] tmp;
     return VCT_OK;

@@ -25,6 +25,7 @@ struct Grid {
     uint64_t pyr_texels = 0;
     // K1 state
     long long* accum = nullptr;      // [n^3][8] int64: albedo rgb, normal xyz, count, pad
+    bool accum_packed = false;       // the last K1 packed its sums (r+2^32 g, b+2^32 nx, ny+2^32 nz, count)
     float4* albedo_occ = nullptr;    // [n^3] (albedo rgb, occupancy)
     float4* normal = nullptr;        // [n^3] (unit normal, 0)
     unsigned long long* occ_bits = nullptr;  // [n^3 / 64] occupancy bitmask

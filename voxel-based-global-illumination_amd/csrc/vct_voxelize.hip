@@ -18,6 +18,7 @@
 // (ctx invariant: records, voxels and bits are zero where no bit is set).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "vct_internal.h"
 
@@ -58,7 +59,7 @@ __global__ void __launch_bounds__(256) k1_tri_setup(
     uint32_t n_tex, int n, float g0x, float g0y, float g0z,
     float inv_h, TriGeom* __restrict__ geom, TriFix* __restrict__ fixo, TriUV* __restrict__ tuv,
     unsigned long long* __restrict__ counts, float4* __restrict__ mesh_tri, float4* __restrict__ mesh_uv,
-    int* __restrict__ err) {
+    int* __restrict__ err, uint32_t* __restrict__ maxabs) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_tri) return;
     uint32_t vi[3] = {idx[3 * t], idx[3 * t + 1], idx[3 * t + 2]};
@@ -101,6 +102,17 @@ __global__ void __launch_bounds__(256) k1_tri_setup(
     f.fix[5] = (long long)roundf(fn[2] * VCT_FIXED_ONE);
     f.tex = tex;
     f.pad = 0;
+    {   // the largest |fixed-point value| a hit of this triangle adds (a textured albedo
+        // Kd x T with T <= 1 rounds to at most Kd's); clamped at 2^31
+        unsigned long long mx = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const unsigned long long a = (unsigned long long)(f.fix[i] < 0 ? -f.fix[i] : f.fix[i]);
+            mx = a > mx ? a : mx;
+        }
+        const uint32_t m32 = mx >= (1ull << 31) ? (1u << 31) : (uint32_t)mx;
+        if (m32 > __hip_atomic_load(maxabs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(maxabs, m32);
+    }
     if (tex >= 0) {
         TriUV r;
 #pragma unroll
@@ -258,7 +270,12 @@ __global__ void __launch_bounds__(256) k1_bucket_starts(const unsigned long long
     for (unsigned long long b = (lo + kCandBucket - 1) / kCandBucket; b * kCandBucket < hi; ++b) starts[b] = t;
 }
 
-// one lane = kCandPerThread consecutive (triangle, voxel) candidates
+// one lane = kCandPerThread consecutive (triangle, voxel) candidates.  PACKED: a hit adds
+// its six 16.16 values as three 64-bit words, r + 2^32 g, b + 2^32 nx, ny + 2^32 nz, plus
+// the count (4 atomics instead of 7; K1 is bound by the L2's atomic rate).  The integer
+// sums are the same: a word's total is sum(lo) + 2^32 sum(hi) mod 2^64, which gives both
+// sums back exactly while |sum| < 2^31 -- k1_resolve checks count x max|value| for that.
+template <bool PACKED>
 __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__ geom,
                                                      const TriFix* __restrict__ fixr,
                                                      const unsigned long long* __restrict__ offs,
@@ -313,11 +330,17 @@ __global__ void __launch_bounds__(256) k1_candidates(const TriGeom* __restrict__
             fa[1] = (long long)roundf((r.kd[1] * tg) * VCT_FIXED_ONE);
             fa[2] = (long long)roundf((r.kd[2] * tb) * VCT_FIXED_ONE);
         }
+        if constexpr (PACKED) {
+            atomicAdd(a + 0, (unsigned long long)fa[0] + ((unsigned long long)fa[1] << 32));
+            atomicAdd(a + 1, (unsigned long long)fa[2] + ((unsigned long long)f.fix[3] << 32));
+            atomicAdd(a + 2, (unsigned long long)f.fix[4] + ((unsigned long long)f.fix[5] << 32));
+        } else {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) atomicAdd(a + i, (unsigned long long)fa[i]);
+            for (int i = 0; i < 3; ++i) atomicAdd(a + i, (unsigned long long)fa[i]);
 #pragma unroll
-        for (int i = 3; i < 6; ++i) atomicAdd(a + i, (unsigned long long)f.fix[i]);
-        if (atomicAdd(a + 6, 1ull) == 0ull) atomicOr(occ_bits + (v >> 6), 1ull << (v & 63));   // first hit
+            for (int i = 3; i < 6; ++i) atomicAdd(a + i, (unsigned long long)f.fix[i]);
+        }
+        if (atomicAdd(a + (PACKED ? 3 : 6), 1ull) == 0ull) atomicOr(occ_bits + (v >> 6), 1ull << (v & 63));   // first hit
     }
 }
 
@@ -341,26 +364,52 @@ __global__ void __launch_bounds__(256) k1_clear(const uint32_t* __restrict__ lis
     }
 }
 
-// K1 resolve: accumulators -> albedo/occupancy, normal of the voxels K1 hit (the
-// occupied list k2_list builds from their bits; the other voxels stay zero)
-__device__ __forceinline__ void resolve_voxel(const long long* __restrict__ accum, size_t v,
-                                              float4* __restrict__ albedo_occ, float4* __restrict__ normal);
-
-__global__ void __launch_bounds__(256) k1_resolve(const long long* __restrict__ accum,
-                                                  const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list,
-                                                  float4* __restrict__ albedo_occ, float4* __restrict__ normal) {
-    const uint32_t cnt = *n_list;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256)
-        resolve_voxel(accum, list[i], albedo_occ, normal);
+// a packed word's two sums (|sum| < 2^31 each)
+__host__ __device__ __forceinline__ void unpack_sums(long long w, long long& lo, long long& hi) {
+    lo = (long long)(int32_t)(uint32_t)(unsigned long long)w;
+    hi = (long long)(((unsigned long long)w - (unsigned long long)lo)) >> 32;
 }
 
+// K1 resolve: accumulators -> albedo/occupancy, normal of the voxels K1 hit (the
+// occupied list k2_list builds from their bits; the other voxels stay zero).  PACKED: a
+// voxel whose count x max|value| could reach 2^31 raises *overflow instead (the host then
+// repeats the voxelization unpacked)
+template <bool PACKED>
 __device__ __forceinline__ void resolve_voxel(const long long* __restrict__ accum, size_t v,
-                                              float4* __restrict__ albedo_occ, float4* __restrict__ normal) {
+                                              float4* __restrict__ albedo_occ, float4* __restrict__ normal,
+                                              uint32_t maxabs, int* __restrict__ overflow);
+
+template <bool PACKED>
+__global__ void __launch_bounds__(256) k1_resolve(const long long* __restrict__ accum,
+                                                  const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list,
+                                                  float4* __restrict__ albedo_occ, float4* __restrict__ normal,
+                                                  const uint32_t* __restrict__ maxabs_p, int* __restrict__ overflow) {
+    const uint32_t cnt = *n_list;
+    const uint32_t maxabs = PACKED ? *maxabs_p : 0u;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256)
+        resolve_voxel<PACKED>(accum, list[i], albedo_occ, normal, maxabs, overflow);
+}
+
+template <bool PACKED>
+__device__ __forceinline__ void resolve_voxel(const long long* __restrict__ accum, size_t v,
+                                              float4* __restrict__ albedo_occ, float4* __restrict__ normal,
+                                              uint32_t maxabs, int* __restrict__ overflow) {
     long long s[7];
     {
         const longlong2* a = (const longlong2*)(accum + 8 * v);
         longlong2 p0 = a[0], p1 = a[1], p2 = a[2], p3 = a[3];
-        s[0] = p0.x; s[1] = p0.y; s[2] = p1.x; s[3] = p1.y; s[4] = p2.x; s[5] = p2.y; s[6] = p3.x;
+        if constexpr (PACKED) {
+            s[6] = p1.y;
+            if ((unsigned long long)s[6] * maxabs >= (1ull << 31)) {
+                atomicOr(overflow, 1);
+                return;
+            }
+            unpack_sums(p0.x, s[0], s[1]);
+            unpack_sums(p0.y, s[2], s[3]);
+            unpack_sums(p1.x, s[4], s[5]);
+        } else {
+            s[0] = p0.x; s[1] = p0.y; s[2] = p1.x; s[3] = p1.y; s[4] = p2.x; s[5] = p2.y; s[6] = p3.x;
+        }
     }
     const unsigned long long cnt = (unsigned long long)s[6];
     double den = (double)cnt * VCT_FIXED_ONE_D;
@@ -380,7 +429,8 @@ __device__ __forceinline__ void resolve_voxel(const long long* __restrict__ accu
 //              words; per word, lane j owns bit j: ballot + mbcnt give coalesced
 //              slots, one atomic per wave);
 //   k2_shade   per occupied voxel: n.l <= 0 -> (0,0,0,1) now, else onto the lit list;
-//   k2_coarse  one bit per (n/64)^3 brick (64^3 bits = 32 KiB);
+//   k2_coarse  one bit per brick of (n/64)^3 voxels (n >= 64; else per voxel), a
+//              64-bit row per (y, z) brick row (at most 64^2 rows = 32 KiB);
 //   k2_walk    per lit voxel the A.3 shadow walk, with the coarse bits in LDS: a
 //              voxel of an empty brick is empty, so its fine word is not read
 //              (same cells, same float sequence, same result).
@@ -482,16 +532,16 @@ __global__ void __launch_bounds__(256) k2_shade(const uint32_t* __restrict__ occ
     }
 }
 
-// coarse occupancy: bit c of brick (bx, by, bz) (brick edge 2^cs) is set when any
-// voxel of it is occupied; cn = n >> cs bricks per axis
+// coarse occupancy: bit bx of 64-bit row (by, bz) (row by + cn bz; brick edge 2^cs, cn =
+// n >> cs <= 64 bricks per axis) is set when any voxel of the brick is occupied
 __global__ void __launch_bounds__(256) k2_coarse(const unsigned long long* __restrict__ bits, int n, int cs,
                                                  uint32_t* __restrict__ coarse) {
     const int cn = n >> cs;
-    const uint32_t c = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t ncb = (uint32_t)cn * cn * cn;
+    const uint32_t c = blockIdx.x * 256 + threadIdx.x;   // bit c = bx + 64 (by + cn bz)
+    const uint32_t ncb = 64u * (uint32_t)cn * cn;
     bool any = false;
-    if (c < ncb) {
-        const int bx = (int)(c % cn), by = (int)((c / cn) % cn), bz = (int)(c / ((uint32_t)cn * cn));
+    if (c < ncb && (int)(c & 63u) < cn) {
+        const int bx = (int)(c & 63u), by = (int)((c >> 6) % cn), bz = (int)((c >> 6) / cn);
         const int e = 1 << cs;
         for (int z = bz * e; z < bz * e + e && !any; ++z)
             for (int y = by * e; y < by * e + e && !any; ++y)
@@ -506,68 +556,77 @@ __global__ void __launch_bounds__(256) k2_coarse(const unsigned long long* __res
     if (c < ncb && (c & 31) == 0) coarse[c >> 5] = (uint32_t)(b >> (threadIdx.x & 32));
 }
 
+constexpr int kCoarseRows = 64 * 64;              // 64-bit rows: 32 KiB of LDS
+
 // A.3 shadow walk with the coarse bits (LDS) in front of the fine word: the
-// dda_visibility() sequence, cell for cell
+// dda_visibility() sequence, cell for cell.  The light direction is uniform, so the
+// step signs and t increments are too.  n = 2^lgn, cn = 2^lgcn coarse cells per axis
+// of edge 2^cs; `bits` covers the n^3 / 8 bytes of the occupancy bit mask (a buffer
+// resource: an out-of-range offset reads 0).
 template <int kB>
-__device__ __forceinline__ float dda_coarse(const unsigned long long* __restrict__ bits, const uint32_t* __restrict__ cb,
-                                            int N, int cs, int cn, float qx, float qy, float qz, float lx, float ly,
+__device__ __forceinline__ float dda_coarse(__amdgpu_buffer_rsrc_t bits, const unsigned long long* __restrict__ cb, int lgn,
+                                            int cs, int lgcn, float qx, float qy, float qz, float lx, float ly,
                                             float lz) {
+    const uint32_t N = 1u << lgn;
     int vx = (int)floorf(qx), vy = (int)floorf(qy), vz = (int)floorf(qz);
-    if (vx < 0 || vy < 0 || vz < 0 || vx >= N || vy >= N || vz >= N) return 1.0f;
-    int sx = lx > 0.0f ? 1 : (lx < 0.0f ? -1 : 0);
-    int sy = ly > 0.0f ? 1 : (ly < 0.0f ? -1 : 0);
-    int sz = lz > 0.0f ? 1 : (lz < 0.0f ? -1 : 0);
+    if (max(max((uint32_t)vx, (uint32_t)vy), (uint32_t)vz) >= N) return 1.0f;
+    const int sx = lx > 0.0f ? 1 : (lx < 0.0f ? -1 : 0);
+    const int sy = ly > 0.0f ? 1 : (ly < 0.0f ? -1 : 0);
+    const int sz = lz > 0.0f ? 1 : (lz < 0.0f ? -1 : 0);
     const float inf = __builtin_inff();
-    float tdx = sx ? 1.0f / fabsf(lx) : inf;
-    float tdy = sy ? 1.0f / fabsf(ly) : inf;
-    float tdz = sz ? 1.0f / fabsf(lz) : inf;
+    const float tdx = sx ? 1.0f / fabsf(lx) : inf;
+    const float tdy = sy ? 1.0f / fabsf(ly) : inf;
+    const float tdz = sz ? 1.0f / fabsf(lz) : inf;
     float tmx = sx > 0 ? ((float)(vx + 1) - qx) * tdx : (sx < 0 ? (qx - (float)vx) * tdx : inf);
     float tmy = sy > 0 ? ((float)(vy + 1) - qy) * tdy : (sy < 0 ? (qy - (float)vy) * tdy : inf);
     float tmz = sz > 0 ? ((float)(vz + 1) - qz) * tdz : (sz < 0 ? (qz - (float)vz) * tdz : inf);
     // batches of kB cells: the walk itself (integer cells, the float t sequence)
-    // does not depend on the lookups, so a batch's cells are stepped first,
-    // branch-free (selects, no exec-mask branches), then looked up together.
-    // A cell counts only while the walk is inside the grid; any occupied counted
-    // cell blocks the light (the walk stops at the first one either way).
+    // does not depend on the lookups, so a batch's cells are stepped first, branch-free,
+    // with their coarse bits, then the fine words of the coarse-occupied ones are looked
+    // up together.  The walk is not frozen where it leaves the grid: every axis moves
+    // one way, so once outside it stays outside, and a cell counts only while inside.
     for (;;) {
-        uint32_t cv[kB], cc[kB];
-        bool in[kB];
-        bool out = false;
+        uint32_t cv[kB], co = 0u;
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
-            in[b] = !out;
-            cv[b] = (uint32_t)vx + (uint32_t)N * ((uint32_t)vy + (uint32_t)N * (uint32_t)vz);
-            cc[b] = (uint32_t)(vx >> cs) + (uint32_t)cn * ((uint32_t)(vy >> cs) + (uint32_t)cn * (uint32_t)(vz >> cs));
-            const bool bx = tmx <= tmy && tmx <= tmz;
-            const bool by = !bx && tmy <= tmz;
+            const uint32_t ux = (uint32_t)vx, uy = (uint32_t)vy, uz = (uint32_t)vz;
+            const bool in = max(max(ux, uy), uz) < N;
+            cv[b] = ux | (uy << lgn) | (uz << (2 * lgn));
+            // unconditional LDS read (an outside cell's row wrapped into the table; its bit
+            // is dropped): a select on the address becomes an exec-mask branch that waits
+            // for every cell's read on its own
+            const unsigned long long row = cb[((uy >> cs) | ((uz >> cs) << lgcn)) & (uint32_t)(kCoarseRows - 1)];
+            co |= ((uint32_t)(row >> ((ux >> cs) & 63u)) & (uint32_t)in) << b;
+            // the spec's choice (x if tmx <= tmy, tmz; else y if tmy <= tmz; else z) from the
+            // minimum: no t is NaN
+            const float tmin = fminf(fminf(tmx, tmy), tmz);
+            const bool bx = tmx == tmin;
+            const bool by = !bx && tmy == tmin;
             const bool bz = !bx && !by;
             const float nx = tmx + tdx, ny = tmy + tdy, nz = tmz + tdz;
-            if (!out) {                                  // freeze the walk once it has left
-                vx += bx ? sx : 0;
-                vy += by ? sy : 0;
-                vz += bz ? sz : 0;
-                tmx = bx ? nx : tmx;
-                tmy = by ? ny : tmy;
-                tmz = bz ? nz : tmz;
-                out = (uint32_t)vx >= (uint32_t)N || (uint32_t)vy >= (uint32_t)N || (uint32_t)vz >= (uint32_t)N;
+            vx += bx ? sx : 0;
+            vy += by ? sy : 0;
+            vz += bz ? sz : 0;
+            tmx = bx ? nx : tmx;
+            tmy = by ? ny : tmy;
+            tmz = bz ? nz : tmz;
+        }
+        // fine words only when some lane of the wave met a coarse-occupied cell; a cell
+        // whose coarse bit is clear reads past the buffer (0)
+        if (__builtin_amdgcn_ballot_w64(co != 0u)) {
+            uint32_t hit = 0u;
+#pragma unroll
+            for (int b = 0; b < kB; ++b) {
+                const uint32_t off = (co >> b) & 1u ? (cv[b] >> 6) << 3 : 0x80000000u;
+                const auto w = __builtin_amdgcn_raw_buffer_load_b64(bits, off, 0, 0);
+                const unsigned long long wd = ((unsigned long long)w[1] << 32) | w[0];
+                hit |= (uint32_t)(wd >> (cv[b] & 63u));
             }
+            if (hit & 1u) return 0.0f;
         }
-        bool blocked = false;
-        unsigned long long wd[kB];
-#pragma unroll
-        for (int b = 0; b < kB; ++b) {
-            const bool co = in[b] && ((cb[in[b] ? cc[b] >> 5 : 0] >> (cc[b] & 31)) & 1u);
-            wd[b] = bits[co ? cv[b] >> 6 : 0];
-            wd[b] = co ? wd[b] : 0ull;
-        }
-#pragma unroll
-        for (int b = 0; b < kB; ++b) blocked |= ((wd[b] >> (cv[b] & 63)) & 1ull) != 0ull;
-        if (blocked) return 0.0f;
-        if (out) return 1.0f;
+        if (max(max((uint32_t)vx, (uint32_t)vy), (uint32_t)vz) >= N) return 1.0f;
     }
 }
-
-constexpr int kCoarseWords = 64 * 64 * 64 / 32;   // 32 KiB of LDS
 
 // one lane per lit voxel; BS-thread blocks share one LDS copy of the coarse bits; KB cells
 // per lookup batch
@@ -579,20 +638,24 @@ __global__ void __launch_bounds__(BS) k2_walk(const uint32_t* __restrict__ lit, 
                                                 const unsigned long long* __restrict__ bits, int n, float lx,
                                                 float ly, float lz, float cr, float cg, float cb,
                                                 float4* __restrict__ r0) {
-    __shared__ uint32_t cbits[kCoarseWords];
-    const int cn = n >> cs;
-    const uint32_t ncw = ((uint32_t)cn * cn * cn + 31) / 32;
-    for (uint32_t i = threadIdx.x; i < ncw; i += BS) cbits[i] = coarse[i];
-    __syncthreads();
+    __shared__ unsigned long long cbits[kCoarseRows];
     const uint32_t cnt = *n_lit;
+    if (blockIdx.x * BS >= cnt) return;           // block-uniform: no lit voxel for this block
+    const int cn = n >> cs;
+    const int lgn = __builtin_ctz((uint32_t)n), lgcn = lgn - cs;
+    const uint32_t nrow = (uint32_t)cn * cn;
+    const unsigned long long* crow = reinterpret_cast<const unsigned long long*>(coarse);
+    for (uint32_t i = threadIdx.x; i < nrow; i += BS) cbits[i] = crow[i];
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t br =
+        __builtin_amdgcn_make_buffer_rsrc((void*)bits, (short)0, (int)(((size_t)n * n * n) >> 3), 0x00020000);
     for (uint32_t i = blockIdx.x * BS + threadIdx.x; i < cnt; i += gridDim.x * BS) {
         const uint32_t v = lit[i];
         const float4 ao = albedo_occ[v];
         const float4 nm = normal[v];
         const float ndl = dot3(nm.x, nm.y, nm.z, lx, ly, lz);
-        const int x = (int)(v % (uint32_t)n), y = (int)((v / (uint32_t)n) % (uint32_t)n),
-                  z = (int)(v / ((uint32_t)n * (uint32_t)n));
-        const float vis = dda_coarse<KB>(bits, cbits, n, cs, cn, ((float)x + 0.5f) + nm.x, ((float)y + 0.5f) + nm.y,
+        const int x = (int)(v & (uint32_t)(n - 1)), y = (int)((v >> lgn) & (uint32_t)(n - 1)), z = (int)(v >> (2 * lgn));
+        const float vis = dda_coarse<KB>(br, cbits, lgn, cs, lgcn, ((float)x + 0.5f) + nm.x, ((float)y + 0.5f) + nm.y,
                                      ((float)z + 0.5f) + nm.z, lx, ly, lz);
         r0[l0_texel(v, (uint32_t)n)] =
             make_float4(((ao.x * cr) * ndl) * vis, ((ao.y * cg) * ndl) * vis, ((ao.z * cb) * ndl) * vis, 1.0f);
@@ -625,17 +688,19 @@ __global__ void __launch_bounds__(256) k2_inject(const float4* __restrict__ albe
     *dst = out;
 }
 
-}  // namespace
-
-hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
-                           uint32_t n_verts, const uint32_t* d_idx, uint32_t n_tri, const uint32_t* d_mat,
-                           const float4* d_kd, uint32_t n_mat, const int32_t* d_map, uint32_t uv_offset,
-                           int* d_err) {
+// One voxelization pass.  packed: try the packed accumulators (k1_candidates); when
+// their exactness bound cannot be shown on the host (more triangles than 2^31 / max|value|)
+// the pass reads back k1_resolve's overflow flag and sets *redo if it fired.
+hipError_t voxelize_pass(vct_ctx* c, const void* d_verts, uint32_t stride, uint32_t n_verts, const uint32_t* d_idx,
+                         uint32_t n_tri, const uint32_t* d_mat, const float4* d_kd, uint32_t n_mat,
+                         const int32_t* d_map, uint32_t uv_offset, int* d_err, bool packed, bool* redo) {
     Grid& g = c->grid;
+    *redo = false;
     hipStream_t s = c->stream;
     const size_t nv = (size_t)g.n * g.n * g.n;
     hipError_t e;
-    // scratch layout: geom | fix | counts | offsets | tile sums | total | textured triangles' UVs
+    // scratch layout: geom | fix | counts | offsets | tile sums | total, max|value|, overflow |
+    // textured triangles' UVs
     const uint32_t n_tiles = (n_tri + kScanTile - 1) / kScanTile;
     size_t off_geom = 0;
     size_t off_fix = off_geom + sizeof(TriGeom) * (size_t)n_tri;
@@ -654,6 +719,8 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
     unsigned long long* offs = (unsigned long long*)(base + off_offs);
     unsigned long long* tiles = (unsigned long long*)(base + off_tiles);
     unsigned long long* total = (unsigned long long*)(base + off_total);
+    uint32_t* maxabs = (uint32_t*)(base + off_total + 8);
+    int* overflow = (int*)(base + off_total + 12);
     TriUV* tuv = d_map ? (TriUV*)(base + off_uv) : nullptr;
 
     // sparse reset of the previous voxelization (its occupied list), then the bits
@@ -663,20 +730,30 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
                        g.normal, g.pyr, g.n);
     if ((e = hipMemsetAsync(g.occ_bits, 0, nwords * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(g.occ_count, 0, 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(total, 0, 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(total, 0, 16, s)) != hipSuccess) return e;   // total, max|value|, overflow
+    bool use_packed = false, check = false;
     if (n_tri > 0) {
         hipLaunchKernelGGL(k1_tri_setup, dim3((n_tri + 255) / 256), dim3(256), 0, s,
                            (const char*)d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat, d_map,
                            uv_offset, c->tex.n, (int)g.n, g.g0[0], g.g0[1], g.g0[2], g.inv_h, geom, fix, tuv, cnt,
-                           c->mesh.tri, c->mesh.uv, d_err);
+                           c->mesh.tri, c->mesh.uv, d_err, maxabs);
         hipLaunchKernelGGL(k_scan_tiles, dim3(n_tiles), dim3(kScanBlock), 0, s, cnt, offs, tiles, n_tri);
         hipLaunchKernelGGL(k_scan_carry, dim3(1), dim3(kScanBlock), 0, s, tiles, n_tiles, total);
         hipLaunchKernelGGL(k_scan_add, dim3(n_tiles), dim3(kScanBlock), 0, s, offs, tiles, n_tri);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         // the candidate total is only known on the device: read it back to size the grid
-        unsigned long long h_total = 0;
-        if ((e = hipMemcpyAsync(&h_total, total, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        // (with the largest |value| a hit adds)
+        unsigned long long h_head[2] = {0, 0};
+        if ((e = hipMemcpyAsync(h_head, total, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        const unsigned long long h_total = h_head[0];
+        const uint32_t h_maxabs = (uint32_t)h_head[1];
+        // a voxel's count never exceeds n_tri: count x max|value| < 2^31 is then certain;
+        // otherwise packed runs with the overflow check (unless a handful of hits could
+        // already overflow: unpacked outright)
+        const unsigned long long safe = h_maxabs ? ((1ull << 31) - 1) / h_maxabs : ~0ull;
+        use_packed = packed && safe >= 256;
+        check = use_packed && n_tri > safe;
         if (h_total > 0) {
             unsigned long long threads = (h_total + kCandPerThread - 1) / kCandPerThread;
             unsigned long long blocks = (threads + 255) / 256;
@@ -687,17 +764,56 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
             uint32_t* starts = (uint32_t*)bp;
             hipLaunchKernelGGL(k1_bucket_starts, dim3((n_tri + 255) / 256), dim3(256), 0, s, offs, n_tri, total,
                                starts);
-            hipLaunchKernelGGL(k1_candidates, dim3((uint32_t)blocks), dim3(256), 0, s, geom, fix, offs,
-                               n_tri, total, (int)g.n, g.accum, g.occ_bits, starts, tuv, c->tex.texels,
-                               c->tex.desc);
+            if (use_packed)
+                hipLaunchKernelGGL(k1_candidates<true>, dim3((uint32_t)blocks), dim3(256), 0, s, geom, fix, offs,
+                                   n_tri, total, (int)g.n, g.accum, g.occ_bits, starts, tuv, c->tex.texels,
+                                   c->tex.desc);
+            else
+                hipLaunchKernelGGL(k1_candidates<false>, dim3((uint32_t)blocks), dim3(256), 0, s, geom, fix, offs,
+                                   n_tri, total, (int)g.n, g.accum, g.occ_bits, starts, tuv, c->tex.texels,
+                                   c->tex.desc);
         }
     }
     // the occupied list (kept for the next reset and for K2), then resolve it
     hipLaunchKernelGGL(k2_list, dim3((uint32_t)((nwords + 255) / 256)), dim3(256), 0, s, g.occ_bits, nwords,
                        g.occ_list, g.occ_count);
-    hipLaunchKernelGGL(k1_resolve, dim3(lb), dim3(256), 0, s, g.accum, g.occ_list, g.occ_count, g.albedo_occ,
-                       g.normal);
-    return hipGetLastError();
+    g.accum_packed = use_packed;
+    if (use_packed)
+        hipLaunchKernelGGL(k1_resolve<true>, dim3(lb), dim3(256), 0, s, g.accum, g.occ_list, g.occ_count,
+                           g.albedo_occ, g.normal, maxabs, overflow);
+    else
+        hipLaunchKernelGGL(k1_resolve<false>, dim3(lb), dim3(256), 0, s, g.accum, g.occ_list, g.occ_count,
+                           g.albedo_occ, g.normal, maxabs, overflow);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (check) {
+        int h_over = 0;
+        if ((e = hipMemcpyAsync(&h_over, overflow, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        *redo = h_over != 0;
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
+// K1.  Packed accumulators by default (VCT_K1_PACKED=0: the seven-atomic form, for A/B);
+// a pass whose packed sums could have overflowed is repeated unpacked (its occupied list
+// drives the repeat's sparse reset), so the result is the same either way.
+hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
+                           uint32_t n_verts, const uint32_t* d_idx, uint32_t n_tri, const uint32_t* d_mat,
+                           const float4* d_kd, uint32_t n_mat, const int32_t* d_map, uint32_t uv_offset,
+                           int* d_err) {
+    static const bool packed = [] {
+        const char* v = getenv("VCT_K1_PACKED");
+        return !(v && strcmp(v, "0") == 0);
+    }();
+    bool redo = false;
+    hipError_t e = voxelize_pass(c, d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat, d_map, uv_offset,
+                                 d_err, packed, &redo);
+    if (e == hipSuccess && redo)
+        e = voxelize_pass(c, d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat, d_map, uv_offset, d_err,
+                          false, &redo);
+    return e;
 }
 
 hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb) {
@@ -712,7 +828,7 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
     // one lane per occupied / lit voxel (n^3 <= 2^30: 32-bit entries)
     int cs = 0;
     while ((g.n >> cs) > 64) ++cs;
-    const uint32_t cn = g.n >> cs, ncw = (cn * cn * cn + 31) / 32;
+    const uint32_t cn = g.n >> cs, ncw = 2 * cn * cn;   // 64-bit rows
     void* sp = nullptr;
     hipError_t e = scratch_get(c, 4, 256 + nv * 4 + (size_t)ncw * 4, &sp);
     if (e != hipSuccess) return e;
@@ -727,7 +843,7 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
         if ((e = hipMemsetAsync(g.pyr, 0, nv * sizeof(float4), s)) != hipSuccess) return e;
         g.l0_dense = false;
     }
-    hipLaunchKernelGGL(k2_coarse, dim3((cn * cn * cn + 255) / 256), dim3(256), 0, s, g.occ_bits, (int)g.n, cs,
+    hipLaunchKernelGGL(k2_coarse, dim3((64 * cn * cn + 255) / 256), dim3(256), 0, s, g.occ_bits, (int)g.n, cs,
                        coarse);
     const uint32_t blocks = (uint32_t)std::min<size_t>((nv / 64 + 255) / 256 + 1, 4096);
     hipLaunchKernelGGL(k2_shade, dim3(blocks), dim3(256), 0, s, g.occ_list, g.occ_count, g.normal, lx, ly, lz, lit,
