@@ -871,6 +871,8 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
         case 40256: VCT_K2_WALK_LAUNCH(4, 256); break;
         case 41024: VCT_K2_WALK_LAUNCH(4, 1024); break;
         case 81024: VCT_K2_WALK_LAUNCH(8, 1024); break;
+        case 320256: VCT_K2_WALK_LAUNCH(32, 256); break;
+        case 80128: VCT_K2_WALK_LAUNCH(8, 128); break;
         default: VCT_K2_WALK_LAUNCH(16, 256); break;
     }
 #undef VCT_K2_WALK_LAUNCH
