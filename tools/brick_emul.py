@@ -35,6 +35,11 @@ def main():
     ap.add_argument("--waves", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--wide", type=int, default=1)
+    ap.add_argument("--nzfit", type=int, default=0,
+                    help="1: a level-A miss fits / clusters only the lanes whose footprint may be nonzero")
+    ap.add_argument("--multi", type=int, default=0,
+                    help="K >= 2: a miss that fits no single 4^3 brick is covered by up to K "
+                         "4^3 bricks (greedy lane clusters) in iso / combined-face mode")
     a = ap.parse_args()
     from oracle import oracle as O
     from vct import Context, _lib, scenes
@@ -111,6 +116,28 @@ def main():
 
     stats = {}
 
+    def cover_bricks(c, alive, negax, sel, K, dkey=None):
+        """bricks of the greedy cover (K + 1: none within K) per wave of sel: take the first
+        remaining lane f, the lanes within 2 of it on every axis, their brick origin (min,
+        or max - 2 toward -axis), the lanes that fit it; repeat on the rest"""
+        out = np.zeros(Wn, np.int64)
+        for wv in np.nonzero(sel)[0]:
+            rem = alive[wv].copy()
+            cw = c[wv]
+            k = 0
+            while rem.any() and k <= K:
+                f = np.argmax(rem)
+                near = rem & np.all(np.abs(cw - cw[f]) <= 2, -1)
+                if dkey is not None:                 # the cluster also shares one direction (comb mode)
+                    near &= np.all(dkey[wv] == dkey[wv, f], -1)
+                lo_, hi_ = cw[near].min(0), cw[near].max(0)
+                org = np.where(negax[wv], hi_ - 2, lo_)
+                fit = near & np.all((cw >= org) & (cw <= org + 2), -1)
+                rem &= ~fit
+                k += 1
+            out[wv] = k if not rem.any() else K + 1
+        return out
+
     def bump(key, m):
         stats[key] = stats.get(key, 0) + int(m.sum())
 
@@ -121,7 +148,8 @@ def main():
         sgnf = np.where(V[..., None], np.sign(np.where(d >= 0, 1, -1)), 0)
         nfaces = (np.any(sgnf > 0, 1) | False).sum(-1) + np.any(sgnf < 0, 1).sum(-1)
         uni &= nfaces == 3
-        negax = np.all((d < 0) | ~V[..., None], 1)             # [W, 3] the cone moves toward -axis
+        negax = np.all((d < 0) | ~V[..., None], 1)
+        dkey = np.concatenate([(d32 * d32).view(np.uint32), (d32 < 0)], -1)             # [W, 3] the cone moves toward -axis
         alpha = np.zeros(V.shape)
         alive = V.copy()
         # cache: level, origin [W,3], size (4 or 6) per entry
@@ -165,10 +193,22 @@ def main():
                 bump(lk + " empty", empty)
                 miss &= ~empty
                 faces_ok = (lvl == 0) | uni | (nfaces <= 4)
+                fitl = alive & ~zl if (isA and a.nzfit) else alive       # lanes that must fit
+                lo = np.where(fitl[..., None], c, BIG).min(1)
+                hi = np.where(fitl[..., None], c, -BIG).max(1)
+                span = hi - lo
                 wide_ok = (lvl == 0) | uni
                 f4 = miss & faces_ok & np.all(span <= 2, -1)
                 f6 = miss & ~f4 & wide_ok & np.all(span <= 4, -1) & bool(a.wide)
                 g = miss & ~f4 & ~f6
+                if a.multi >= 2:
+                    # level 0 / dir_uniform waves: any lane cluster; else clusters of one direction
+                    kb = np.where(wide_ok, cover_bricks(c, fitl, negax, g & wide_ok, a.multi),
+                                  cover_bricks(c, fitl, negax, g & ~wide_ok, a.multi, dkey)
+                                  if lvl > 0 else a.multi + 1)
+                    for k_ in range(2, a.multi + 1):
+                        bump(lk + f" stage4x{k_}", kb == k_)
+                    g &= ~((kb >= 2) & (kb <= a.multi))
                 bump(lk + " stage4", f4)
                 bump(lk + " stage6", f6)
                 bump(lk + " gather", g)

@@ -69,7 +69,7 @@ def main():
         if not a.clk:
             print(f"  level B: hit {c[26]} / staged {c[27]} / gather {c[28]} / not sampled {c[31]}; "
                   f"faces-mode brick samples A {c[29]} / B {c[30]}")
-            print(f"  empty-space maps: level-A misses skipped {c[40]} / level-B misses skipped {c[41]}")
+            print(f"  empty-space maps: level-A misses skipped {c[40]}; cluster covers: level A {c[41]} / level B {c[42]}")
         print(f"  wave-steps: table {c[44]} / per-lane {c[46]}; active lanes {c[45]} "
               f"({c[45] / max(c[44] + c[46], 1):.1f} per wave-step), valid-pixel lanes {c[47] / max(c[44] + c[46], 1):.1f}")
         print(f"  gather reasons: faces not uniform {c[16]}; footprint span (level 0) <=3/<=5/<=9/more {c[18:22]}"
