@@ -491,7 +491,26 @@ def load_relight_profile(n, scene):
     return rec, None
 
 
-def relight_roofline(ctx, n, scene, k1_ms, k2_ms, k3_ms):
+def k3_relight_bytes(ao_alpha, n):
+    """Algorithmic bytes of a relight K3 build (Grid::k3_live, vct_mips.hip): the first
+    launch reads level 0 and writes levels 1..3 only for its blocks of 16 x 16 x 2 BZ
+    level-0 voxels that hold an occupied voxel (BZ = VCT_K3_BZ, 4 by default); the later
+    launches read level 3 and write levels 4..L whole.  -> (bytes, live block fraction)"""
+    import numpy as np
+    L = int(math.log2(n))
+    bz = int(os.environ.get("VCT_K3_BZ", "4"))
+    bz = bz if bz in (2, 8) else 4
+    occ = ao_alpha > 0                                  # [z][y][x]
+    zb = 2 * bz
+    live = occ.reshape(n // zb, zb, n // 16, 16, n // 16, 16).any(axis=(1, 3, 5))
+    frac = float(live.mean())
+    top = min(3, L)
+    first = n ** 3 * 16 + sum(6 * (n >> l) ** 3 * 16 for l in range(1, top + 1))
+    rest = (6 * (n >> top) ** 3 * 16 + sum(6 * (n >> l) ** 3 * 16 for l in range(top + 1, L + 1))) if L > top else 0
+    return int(frac * first + rest), frac
+
+
+def relight_roofline(ctx, n, scene, k1_ms, k2_ms, k3_ms, k3_sparse=False):
     """Rooflines of the relight kernels.  From the rocprofv3 record of this build (per call:
     VALU wave-instructions, HBM bytes = (2 FETCH_SIZE + WRITE_SIZE) x 1024 and, for K1, the
     L2's atomic requests x 64 B) three rates are formed over the stage's kernel time --
@@ -506,6 +525,10 @@ def relight_roofline(ctx, n, scene, k1_ms, k2_ms, k3_ms):
     L = int(math.log2(n))
     k3_bytes = n ** 3 * 16 + sum(6 * (n >> l) ** 3 * 16 for l in range(1, L + 1))
     ao, _ = ctx.download_voxels()
+    k3_live = None
+    if k3_sparse and n >= 16 and os.environ.get("VCT_K3_SPARSE", "1") != "0":
+        # a relight build skips K3's blocks without an occupied voxel: count only the rest
+        k3_bytes, k3_live = k3_relight_bytes(ao[..., 3], n)
     occ = int(np.count_nonzero(ao[..., 3] > 0))
     k2_bytes = occ * 48
     rec, reason = load_relight_profile(n, scene)
@@ -539,6 +562,10 @@ def relight_roofline(ctx, n, scene, k1_ms, k2_ms, k3_ms):
                   "profile_tag": st.get("tag")})
         out[f"{name}_roofline"] = r
     out["k2_roofline"]["occupied_voxels"] = occ
+    out["k3_roofline"]["build"] = ("relight (K2 level 0, same occupancy: blocks without an occupied voxel "
+                                   "and the K4 maps skipped)" if k3_live is not None else "full")
+    if k3_live is not None:
+        out["k3_roofline"]["live_block_frac"] = round(k3_live, 4)
     return out
 
 
@@ -606,7 +633,9 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     k3_ms = timed_queued(ctx.build_mips)
     r.update({"k2_inject_ms": round(k2_ms, 3), "k3_mips_ms": round(k3_ms, 3), "grid_bcast_ms": round(bcast_ms, 3)})
     if relight_roofs:
-        r.update(relight_roofline(ctx, n, scene_name, r["k1_voxelize_ms"], k2_ms, k3_ms))
+        # world 1: level 0 comes from K2 here, so the timed builds are relight builds; with
+        # more ranks it arrived through set_level0_from_device (a dense write: full builds)
+        r.update(relight_roofline(ctx, n, scene_name, r["k1_voxelize_ms"], k2_ms, k3_ms, k3_sparse=world == 1))
 
     cam = Camera()
     eye = [float(x) for x in cam.position]

@@ -224,6 +224,61 @@ def test_trace_parity(gpu_ready, oracle_mod, name, n, kind, aniso, nd, spec):
     ctx.close()
 
 
+@pytest.mark.parametrize("n", [16, 64, 128])
+def test_mips_relight_sparse_bitexact(gpu_ready, oracle_mod, n):
+    """Relight builds (Grid::k3_live): after K2 level 0 is nonzero exactly at the occupied
+    voxels, so a build that follows another from the same occupancy skips K3's blocks
+    without an occupied voxel and the K4 maps.  A light sequence, a scene change (K1 ->
+    full build), a dense upload in between (full build) and back: every pyramid equals
+    the oracle's, and frames traced after a skipping build equal a fresh context's."""
+    from vct import Context, scenes
+    from helpers import scene_arrays
+    g0, E = scenes.grid_for_unit_box(n)
+    lights = [scenes.LIGHT_DIR, (0.3, 0.9, -0.2), (-0.5, 0.4, 0.6)]
+    w, h = 64, 48
+    rng = np.random.default_rng(5 + n)
+    pos = np.zeros((h, w, 4), np.float32)
+    pos[..., :3] = np.array(g0, np.float32) + rng.uniform(0.1, 0.9, (h, w, 3)).astype(np.float32) * E
+    pos[..., 3] = 1.0
+    nv = rng.standard_normal((h, w, 3))
+    nrm = np.zeros((h, w, 4), np.float32)
+    nrm[..., :3] = nv / np.linalg.norm(nv, axis=-1, keepdims=True)
+    alb = np.full((h, w, 4), 0.5, np.float32)
+    eye = (0.0, 0.5, 3.0)
+    ctx = Context(n, g0, E)
+
+    def check(name, light, arrays):
+        v, i, m, k = arrays
+        ref = oracle_mod.pipeline(n, g0, E, v, i, m, k, light)
+        assert np.array_equal(ctx.download_level(0), ref["r0"]), (name, light)
+        assert np.array_equal(gpu_pyramid_flat(ctx), ref["pyr"]), (name, light)
+        fresh = Context(n, g0, E)
+        fresh.voxelize(v, i, m, k)
+        fresh.inject_directional(light, scenes.LIGHT_COLOR)
+        fresh.build_mips()
+        a, b = ctx.trace(pos, nrm, alb, eye), fresh.trace(pos, nrm, alb, eye)
+        for key in ("diffuse", "spec", "steps_px"):
+            assert np.array_equal(a[key], b[key]), (name, light, key)
+        fresh.close()
+
+    for name in ("atrium", "cornell"):
+        _, arrays = scene_arrays(name)
+        ctx.voxelize(*arrays)
+        for light in lights:                     # the first build is full, the others skip
+            ctx.inject_directional(light, scenes.LIGHT_COLOR)
+            ctx.build_mips()
+            check(name, light, arrays)
+    # a dense level 0 (no K2): a full build from it, then K2 again
+    ctx.upload_level0(rng.random((n, n, n, 4)).astype(np.float32) * (rng.random((n, n, n, 1)) < 0.1))
+    ctx.build_mips()
+    assert np.array_equal(gpu_pyramid_flat(ctx), oracle_mod.build_mips(n, ctx.download_level(0), True))
+    for light in lights[:2]:
+        ctx.inject_directional(light, scenes.LIGHT_COLOR)
+        ctx.build_mips()
+        check("cornell", light, arrays)
+    ctx.close()
+
+
 @pytest.mark.parametrize("n", [16, 64])
 def test_empty_space_maps_exact(gpu_ready, oracle_mod, n, monkeypatch):
     """K4's empty-space test (Grid::zmap, rebuilt by build_mips from the level-0 texels

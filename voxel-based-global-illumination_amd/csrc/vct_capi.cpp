@@ -212,6 +212,7 @@ vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
         if (e == hipSuccess) e = hipMalloc((void**)&g.occ, ob ? ob : 1);
         if (e == hipSuccess) e = hipMalloc((void**)&g.zmap, (size_t)zw * 4);
     }
+    if (e == hipSuccess) e = hipMalloc((void**)&g.k3_live, nv / 256 > 0 ? nv / 256 : 1);
     if (e == hipSuccess) e = hipMalloc((void**)&g.occ_list, nv * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&g.occ_count, 256);
     if (e == hipSuccess) e = hipMemset(g.occ_count, 0, 256);
@@ -292,6 +293,7 @@ void vct_destroy(vct_ctx* c) {
     if (g.normal) (void)hipFree(g.normal);
     if (g.occ_bits) (void)hipFree(g.occ_bits);
     if (g.occ_list) (void)hipFree(g.occ_list);
+    if (g.k3_live) (void)hipFree(g.k3_live);
     if (g.b0) (void)hipFree(g.b0);
     if (g.occ) (void)hipFree(g.occ);
     if (g.zmap) (void)hipFree(g.zmap);
@@ -390,6 +392,7 @@ static vct_status voxelize_dev(vct_ctx* c, const void* dv, uint32_t stride, uint
     // a grid from out-of-range indices is partial: inject / mips / trace refuse it (VCT_ESTATE)
     c->grid.voxelized = herr == 0;
     c->grid.injected = c->grid.mipped = false;
+    c->grid.k3_sparse_ok = false;            // the occupancy changed: next K3 builds every block
     ++c->grid_epoch;
     if (herr) return fail(c, VCT_EINVAL, "vertex, material or diffuse-map index out of range");
     return VCT_OK;

@@ -49,6 +49,16 @@ struct Grid {
     uint32_t zm_rw[kZLevels + 1] = {};       // dwords per row of map m
     int zm_levels = 0;
     bool zm_valid = false;                   // the maps describe the current pyramid
+    // Relight builds (vct_mips.hip launch_mips): after K2, level 0 is nonzero exactly at
+    // the occupied voxels (every one gets alpha 1, every other voxel is +0), a pattern only
+    // K1 changes.  k3_live[b] = 1 iff K3's first-launch block b (k3_live_bz its depth)
+    // holds an occupied voxel.  k3_sparse_ok: the last K3 build ran on such a level 0 for
+    // the current occupancy, so every level >= 1 texel and b0 bit above a non-live block is
+    // +0 / 0 and the K4 maps are current; the next build from a K2 level 0 may then skip
+    // the non-live blocks and the maps.  Cleared by K1 and by any dense level-0 write.
+    uint8_t* k3_live = nullptr;              // [n^3 / 256]
+    int k3_live_bz = 0;
+    bool k3_sparse_ok = false;
     bool voxelized = false, injected = false, mipped = false;
     bool l0_dense = false;   // level 0 was replaced densely (upload / device copy): K2 must clear it whole
     bool l0_on_peers = false;   // multi-device: the other devices hold this level 0 (vct_build_mips copies it)

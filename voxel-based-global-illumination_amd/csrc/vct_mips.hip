@@ -196,12 +196,15 @@ struct BlockK {
     int n, l;                                 // grid edge, first level built
     int brick_writes;                         // level l stored in brick order from LDS (VCT_K3_WRITE)
     uint32_t* b0;                             // level 1 from level 0: the level-0 nonzero bits (Grid::b0), or null
+    const uint8_t* live;                      // relight build: only blocks b with live[b] != 0 (Grid::k3_live), or null
 };
 
 template <int MODE, int BZ>
 __global__ void __launch_bounds__(kBlk * kBlk * BZ) k3_block(const BlockK k) {
     constexpr int kT = kBlk * kBlk * BZ;      // threads: one per parent of a full block
     __shared__ float4 st[kT * 9];
+    // a block without an occupied voxel reads only +0 and its subtree already holds +0
+    if (k.live && !k.live[blockIdx.x]) return;
     constexpr int FACES = MODE == kIso6 ? 6 : 1;
     const int t = (int)threadIdx.x;
     const int f0 = MODE == kFace ? (int)blockIdx.y : 0;
@@ -501,8 +504,22 @@ __global__ void __launch_bounds__(256) k_relayout(const float4* __restrict__ src
 
 }  // namespace
 
+// Grid::k3_live for K3's first launch with blocks of 16 x 16 x 2 BZ level-0 voxels (n >= 16):
+// one lane per occupied voxel of K1's list
+__global__ void __launch_bounds__(256) k3_live_blocks(const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list,
+                                                      uint32_t lgn, uint32_t zsh, uint8_t* __restrict__ live) {
+    const uint32_t cnt = *n_list, mask = (1u << lgn) - 1u, nbk = 1u << (lgn - 4u), nbz = 1u << (lgn - zsh);
+    (void)nbz;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) {
+        const uint32_t v = list[i];
+        const uint32_t x = v & mask, y = (v >> lgn) & mask, z = v >> (2u * lgn);
+        live[(x >> 4) + nbk * ((y >> 4) + nbk * (z >> zsh))] = 1;
+    }
+}
+
 hipError_t launch_mips(vct_ctx* c) {
     Grid& g = c->grid;
+    const bool zm_was_valid = g.zm_valid;
     g.zm_valid = false;
     const char* plan = getenv("VCT_K3_PLAN");
     if (plan && strcmp(plan, "level") == 0) {    // A/B: one lane-per-parent launch per level (no K4 maps)
@@ -541,6 +558,12 @@ hipError_t launch_mips(vct_ctx* c) {
         const int b = v ? atoi(v) : 4;
         return b == 8 || b == 2 ? b : 4;
     }();
+    // Relight build (Grid::k3_live): level 0 from K2 (not a dense write) and the last build
+    // was one too, for this occupancy -- the non-live blocks of the first launch and the K4
+    // maps (built from the same nonzero pattern) are skipped.  VCT_K3_SPARSE=0: A/B without.
+    static const bool sparse_on = !(getenv("VCT_K3_SPARSE") && strcmp(getenv("VCT_K3_SPARSE"), "0") == 0);
+    const bool k2_level0 = !g.l0_dense;
+    const bool sparse = sparse_on && k2_level0 && g.k3_sparse_ok && g.k3_live_bz == bz && g.n >= 16 && zm_was_valid;
     bool built = false;
     for (uint32_t l = 1; l <= g.L;) {
         const uint32_t nl = g.n >> l, E = nl < (uint32_t)kBlk ? nl : (uint32_t)kBlk;
@@ -549,6 +572,7 @@ hipError_t launch_mips(vct_ctx* c) {
         const uint32_t blocks = all;
         k.l = (int)l;
         k.b0 = (l == 1 && g.zm_levels > 0) ? g.b0 : nullptr;   // the launch that reads level 0
+        k.live = (l == 1 && sparse) ? g.k3_live : nullptr;
 #define VCT_K3_LAUNCH(BZv)                                                                                      \
     do {                                                                                                        \
         constexpr uint32_t thr = (uint32_t)(kBlk * kBlk * BZv);                                                \
@@ -560,7 +584,7 @@ hipError_t launch_mips(vct_ctx* c) {
         else if (bz == 2) VCT_K3_LAUNCH(2);
         else VCT_K3_LAUNCH(4);
 #undef VCT_K3_LAUNCH
-        if (k.b0 && !built) {
+        if (k.b0 && !built && !sparse) {
             // level 0's bits are written: the K4 maps (in order on the ctx stream; forked onto a
             // side stream beside K3's top levels it measured slower at 256^3, 0.130 -> 0.139 ms)
             const hipError_t e = launch_zmaps(c, c->stream);
@@ -572,6 +596,18 @@ hipError_t launch_mips(vct_ctx* c) {
     if (built) {
         g.zm_valid = !(getenv("VCT_ZMAP") && strcmp(getenv("VCT_ZMAP"), "0") == 0);   // VCT_ZMAP=0: A/B without
     }
+    if (sparse) g.zm_valid = true;            // same level-0 pattern as when they were built
+    if (k2_level0 && !sparse && g.n >= 16) {
+        // a full build from a K2 level 0: the live blocks of this occupancy, for the next ones
+        const uint32_t lgn = (uint32_t)__builtin_ctz(g.n), zsh = (uint32_t)__builtin_ctz(2 * bz);
+        const size_t nlive = ((size_t)g.n >> 4) * (g.n >> 4) * (g.n >> zsh);
+        hipError_t e = hipMemsetAsync(g.k3_live, 0, nlive, c->stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k3_live_blocks, dim3(1024), dim3(256), 0, c->stream, (const uint32_t*)g.occ_list,
+                           (const uint32_t*)g.occ_count, lgn, zsh, g.k3_live);
+        g.k3_live_bz = bz;
+    }
+    g.k3_sparse_ok = k2_level0;
     return hipGetLastError();
 }
 
