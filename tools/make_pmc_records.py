@@ -96,13 +96,29 @@ def k4_record(passes):
     return rec
 
 
-def stage_records(passes, calls):
-    """per relight stage: counters and kernel time per call, and the per-kernel split"""
+def first_build(disp, st):
+    """dispatch ids of stage st's first call: the earliest dispatch of each (kernel, grid)"""
+    first = {}
+    for did in sorted(disp):
+        e = disp[did]
+        s, _ = stage_of(e["kernel"])
+        if s == st:
+            first.setdefault((e["kernel"], e["grid"]), did)
+    return set(first.values())
+
+
+def stage_records(passes, calls, drop_first=()):
+    """per relight stage: counters and kernel time per call, and the per-kernel split.
+    Stages in drop_first lose their first call (e.g. K3's full build before the relight
+    builds the workload measures; calls[st] counts the calls kept)."""
     out = {}
     for st in STAGES:
         per_kernel = {}
         for p, disp in passes.items():
-            for e in disp.values():
+            skip = first_build(disp, st) if st in drop_first else set()
+            for did, e in disp.items():
+                if did in skip:
+                    continue
                 s, kname = stage_of(e["kernel"])
                 if s != st:
                     continue
@@ -164,8 +180,14 @@ def main():
               f"form {info['form_name']}")
         if info["world"] == 1:
             n_, scene = info["key"].split(" ")[0], info["key"].split(" ")[2]
+            # K3: the first build after K1 is full, the later ones are relight builds (only
+            # the blocks with an occupied voxel, no K4 maps): the record is of those
+            full1 = bool(info.get("k3_first_build_full"))
             st = stage_records(passes, {"k1": info["k1_calls"], "k2": info["relight_calls"],
-                                        "k3": info["relight_calls"]})
+                                        "k3": info["relight_calls"] - (1 if full1 else 0)},
+                               drop_first=("k3",) if full1 else ())
+            if full1 and "k3" in st:
+                st["k3"]["build"] = "relight (first full build after K1 dropped)"
             for s_, v in st.items():
                 v.update({"lib_sha256": sha, "tag": a.tag, "source": os.path.relpath(wdir, REPO)})
                 if "FETCH_SIZE" in v and "WRITE_SIZE" in v:

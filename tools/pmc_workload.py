@@ -6,7 +6,7 @@
 Runs exactly what bench.py runs for that line -- the same scene, grid, frame, cone set,
 G-buffer (the HIP raster from the reference camera; G_rand with seed 42 for `rand`) and
 default variant -- on one GPU: K1 (voxelize_device) x3, K2 (inject) x10, K3 (build_mips)
-x10, one counting K4 launch, the launches the K4 tuner needs to settle (as
+x10 (the first after K1 a full build, the others relight builds), one counting K4 launch, the launches the K4 tuner needs to settle (as
 bench.settle_form), then `--launches` timed K4 launches of the settled form.  With
 --world N it is rank `--rank`'s own launch of the N-rank screen-tile split (compact
 output), the launch bench.py's rank 0 times at N GPUs.  Prints one JSON line (the
@@ -100,7 +100,7 @@ def main():
     print(json.dumps({"key": key, "workload": a.wl, "world": W, "rank": r, "cone_steps": int(cnt[0].item()),
                       "texel_fetches": int(cnt[1].item()), "valid_px": valid_px, "form": form,
                       "form_name": bench.form_name(form), "launches": a.launches, "relight_calls": a.relight,
-                      "k1_calls": 3, "occupied_voxels": None}))
+                      "k1_calls": 3, "occupied_voxels": None, "k3_first_build_full": True}))
     ctx.close()
 
 
