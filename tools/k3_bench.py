@@ -1,4 +1,5 @@
-"""K3 (mip build) timing on one GPU: the atrium at n^3, build_mips `reps` times; run under
+"""K3 (mip build) timing on one GPU: a scene at n^3, one build, then build_mips `reps` times
+(relight builds: Grid::k3_live; VCT_K3_SPARSE=0 full builds); run under
 rocprofv3 --kernel-trace --stats for the per-kernel split (VCT_K3_PLAN=level: one
 lane-per-parent launch per level, for A/B against the block-subtree plan)."""
 import argparse
@@ -14,6 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--scene", default="atrium")
     a = ap.parse_args()
     import torch
     from vct import Context, scenes
@@ -21,7 +23,7 @@ def main():
     ctx = Context(a.n, g0, E)
     st = torch.cuda.current_stream()
     ctx.set_stream(st.cuda_stream)
-    ctx.voxelize(*scenes.atrium().arrays())
+    ctx.voxelize(*scenes.SCENES[a.scene]().arrays())
     ctx.inject_directional(scenes.LIGHT_DIR)
     ctx.build_mips()
     torch.cuda.synchronize()
@@ -31,8 +33,10 @@ def main():
         ctx.build_mips()
     e1.record(st)
     torch.cuda.synchronize()
-    print(f"n={a.n} K3 {e0.elapsed_time(e1) / a.reps:.4f} ms per build "
-          f"({'per-level' if os.environ.get('VCT_K3_PLAN') == 'level' else 'block subtrees'})")
+    sparse = os.environ.get("VCT_K3_SPARSE", "1") != "0"
+    print(f"{a.scene} n={a.n} BZ={os.environ.get('VCT_K3_BZ', '4')} K3 {e0.elapsed_time(e1) / a.reps:.4f} ms per build "
+          f"({'per-level' if os.environ.get('VCT_K3_PLAN') == 'level' else 'block subtrees'}, "
+          f"{'relight builds' if sparse else 'full builds'})")
 
 
 if __name__ == "__main__":

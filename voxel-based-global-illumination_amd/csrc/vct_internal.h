@@ -56,7 +56,9 @@ struct Grid {
     // the current occupancy, so every level >= 1 texel and b0 bit above a non-live block is
     // +0 / 0 and the K4 maps are current; the next build from a K2 level 0 may then skip
     // the non-live blocks and the maps.  Cleared by K1 and by any dense level-0 write.
-    uint8_t* k3_live = nullptr;              // [n^3 / 256]
+    uint8_t* k3_live = nullptr;              // [n^3 / 256] live flag per block
+    uint32_t* k3_live_list = nullptr;        // [n^3 / 1024] + count: the live blocks (any order)
+    uint32_t k3_live_count = 0;              // host copy, read back with K1's error word
     int k3_live_bz = 0;
     bool k3_sparse_ok = false;
     bool voxelized = false, injected = false, mipped = false;
@@ -217,6 +219,9 @@ hipError_t launch_voxelize(vct_ctx* c, const void* d_verts,
 hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb);
 // K3 (and the K4 empty-space maps of Grid::zmap)
 hipError_t launch_mips(vct_ctx* c);
+// K3's live-block list for the occupancy K1 just built (queued on the ctx stream; the count
+// reaches g.k3_live_count at the next stream synchronisation)
+hipError_t launch_k3_live(vct_ctx* c);
 // one nl^3 face volume between the pyramid's texel layout and linear-Z (vct_device.h)
 hipError_t launch_relayout(vct_ctx* c, const float4* src, float4* dst, uint32_t nl, bool to_linear);
 // K4

@@ -196,22 +196,23 @@ struct BlockK {
     int n, l;                                 // grid edge, first level built
     int brick_writes;                         // level l stored in brick order from LDS (VCT_K3_WRITE)
     uint32_t* b0;                             // level 1 from level 0: the level-0 nonzero bits (Grid::b0), or null
-    const uint8_t* live;                      // relight build: only blocks b with live[b] != 0 (Grid::k3_live), or null
+    const uint32_t* live;                     // relight build: workgroup i builds block live[i] (Grid::k3_live_list), or null
 };
 
 template <int MODE, int BZ>
 __global__ void __launch_bounds__(kBlk * kBlk * BZ) k3_block(const BlockK k) {
     constexpr int kT = kBlk * kBlk * BZ;      // threads: one per parent of a full block
     __shared__ float4 st[kT * 9];
-    // a block without an occupied voxel reads only +0 and its subtree already holds +0
-    if (k.live && !k.live[blockIdx.x]) return;
+
     constexpr int FACES = MODE == kIso6 ? 6 : 1;
     const int t = (int)threadIdx.x;
     const int f0 = MODE == kFace ? (int)blockIdx.y : 0;
     const uint32_t nl = (uint32_t)k.n >> k.l, nc = 2u * nl;
     // block of E x E x Ez parents (E = min(8, n_l), Ez = min(BZ, n_l))
     const int E = nl < (uint32_t)kBlk ? (int)nl : kBlk, Ez = nl < (uint32_t)BZ ? (int)nl : BZ, E3 = E * E * Ez;
-    const uint32_t nbk = nl / (uint32_t)E, b = blockIdx.x;
+    // relight build: only the blocks with an occupied voxel (the others read only +0, and
+    // their subtree already holds what this build would write)
+    const uint32_t nbk = nl / (uint32_t)E, b = k.live ? k.live[blockIdx.x] : blockIdx.x;
     const uint32_t X0 = (b % nbk) * E, Y0 = ((b / nbk) % nbk) * E, Z0 = (b / (nbk * nbk)) * Ez;
     // children: face f0 of level l-1 (level 0 for kIso6 and level 1 of kBox)
     const float4* src = k.pyr + k.off[k.l - 1] + (MODE == kFace ? (size_t)f0 * nc * nc * nc : 0);
@@ -505,16 +506,61 @@ __global__ void __launch_bounds__(256) k_relayout(const float4* __restrict__ src
 }  // namespace
 
 // Grid::k3_live for K3's first launch with blocks of 16 x 16 x 2 BZ level-0 voxels (n >= 16):
-// one lane per occupied voxel of K1's list
+// one lane per occupied voxel of K1's list; then the list of the live blocks
 __global__ void __launch_bounds__(256) k3_live_blocks(const uint32_t* __restrict__ list, const uint32_t* __restrict__ n_list,
                                                       uint32_t lgn, uint32_t zsh, uint8_t* __restrict__ live) {
-    const uint32_t cnt = *n_list, mask = (1u << lgn) - 1u, nbk = 1u << (lgn - 4u), nbz = 1u << (lgn - zsh);
-    (void)nbz;
+    const uint32_t cnt = *n_list, mask = (1u << lgn) - 1u, nbk = 1u << (lgn - 4u);
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) {
         const uint32_t v = list[i];
         const uint32_t x = v & mask, y = (v >> lgn) & mask, z = v >> (2u * lgn);
         live[(x >> 4) + nbk * ((y >> 4) + nbk * (z >> zsh))] = 1;
     }
+}
+
+__global__ void __launch_bounds__(256) k3_live_compact(const uint8_t* __restrict__ live, uint32_t nblocks,
+                                                       uint32_t* __restrict__ out, uint32_t* __restrict__ count) {
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
+    const bool on = b < nblocks && live[b] != 0;
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(on);
+    uint32_t base = 0;
+    if ((threadIdx.x & 63u) == 0u && m) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+    if (on) out[base + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63u)) - 1ull))] = b;
+}
+
+// K3's block depth: 8 x 8 x 4 parents (256 threads, 36 KB of LDS, subtrees three levels
+// deep) beat the 8^3 cube (512 threads, 72 KB, four levels) by 4 % at 256^3 and 9 % at
+// 512^3, and 8 x 8 x 2 by 3-4 %: twice the workgroups in flight per CU hide the staging
+// loads better than the one saved launch (relight builds too: tools/k3_shapes.sh).
+// VCT_K3_BZ = 8 | 2 selects the others (A/B).
+static int k3_block_depth() {
+    static const int bz = [] {
+        const char* v = getenv("VCT_K3_BZ");
+        const int b = v ? atoi(v) : 4;
+        return b == 8 || b == 2 ? b : 4;
+    }();
+    return bz;
+}
+
+hipError_t launch_k3_live(vct_ctx* c) {
+    Grid& g = c->grid;
+    g.k3_live_count = 0;
+    if (g.n < 16) return hipSuccess;
+    const int bz = k3_block_depth();
+    const uint32_t lgn = (uint32_t)__builtin_ctz(g.n), zsh = (uint32_t)__builtin_ctz(2 * bz);
+    const uint32_t nblocks = (g.n >> 4) * (g.n >> 4) * (g.n >> zsh);
+    uint32_t* cnt = g.k3_live_list + (g.n / 16u) * (g.n / 16u) * (g.n / 4u);   // past the largest list
+    hipError_t e = hipMemsetAsync(g.k3_live, 0, nblocks, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), c->stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k3_live_blocks, dim3(1024), dim3(256), 0, c->stream, (const uint32_t*)g.occ_list,
+                       (const uint32_t*)g.occ_count, lgn, zsh, g.k3_live);
+    hipLaunchKernelGGL(k3_live_compact, dim3((nblocks + 255) / 256), dim3(256), 0, c->stream,
+                       (const uint8_t*)g.k3_live, nblocks, g.k3_live_list, cnt);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    e = hipMemcpyAsync(&g.k3_live_count, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream);
+    g.k3_live_bz = bz;
+    return e;
 }
 
 hipError_t launch_mips(vct_ctx* c) {
@@ -549,15 +595,7 @@ hipError_t launch_mips(vct_ctx* c) {
     }();
     k.brick_writes = bw;
     k.b0 = nullptr;
-    // block depth: 8 x 8 x 4 parents (256 threads, 36 KB of LDS, subtrees three levels
-    // deep) beat the 8^3 cube (512 threads, 72 KB, four levels) by 4 % at 256^3 and 9 % at
-    // 512^3, and 8 x 8 x 2 by 3-4 %: twice the workgroups in flight per CU hide the staging
-    // loads better than the one saved launch. VCT_K3_BZ = 8 | 2 selects the others (A/B).
-    static const int bz = [] {
-        const char* v = getenv("VCT_K3_BZ");
-        const int b = v ? atoi(v) : 4;
-        return b == 8 || b == 2 ? b : 4;
-    }();
+    const int bz = k3_block_depth();
     // Relight build (Grid::k3_live): level 0 from K2 (not a dense write) and the last build
     // was one too, for this occupancy -- the non-live blocks of the first launch and the K4
     // maps (built from the same nonzero pattern) are skipped.  VCT_K3_SPARSE=0: A/B without.
@@ -569,12 +607,13 @@ hipError_t launch_mips(vct_ctx* c) {
         const uint32_t nl = g.n >> l, E = nl < (uint32_t)kBlk ? nl : (uint32_t)kBlk;
         const uint32_t Ez = nl < (uint32_t)bz ? nl : (uint32_t)bz;
         const uint32_t nbk = nl / E, all = nbk * nbk * (nl / Ez);
-        const uint32_t blocks = all;
         k.l = (int)l;
         k.b0 = (l == 1 && g.zm_levels > 0) ? g.b0 : nullptr;   // the launch that reads level 0
-        k.live = (l == 1 && sparse) ? g.k3_live : nullptr;
+        k.live = (l == 1 && sparse) ? g.k3_live_list : nullptr;
+        const uint32_t blocks = k.live ? g.k3_live_count : all;
 #define VCT_K3_LAUNCH(BZv)                                                                                      \
     do {                                                                                                        \
+        if (blocks == 0) break;                                                                                 \
         constexpr uint32_t thr = (uint32_t)(kBlk * kBlk * BZv);                                                \
         if (!g.aniso) hipLaunchKernelGGL((k3_block<kBox, BZv>), dim3(blocks), dim3(thr), 0, c->stream, k);     \
         else if (l == 1) hipLaunchKernelGGL((k3_block<kIso6, BZv>), dim3(blocks), dim3(thr), 0, c->stream, k); \
@@ -597,16 +636,6 @@ hipError_t launch_mips(vct_ctx* c) {
         g.zm_valid = !(getenv("VCT_ZMAP") && strcmp(getenv("VCT_ZMAP"), "0") == 0);   // VCT_ZMAP=0: A/B without
     }
     if (sparse) g.zm_valid = true;            // same level-0 pattern as when they were built
-    if (k2_level0 && !sparse && g.n >= 16) {
-        // a full build from a K2 level 0: the live blocks of this occupancy, for the next ones
-        const uint32_t lgn = (uint32_t)__builtin_ctz(g.n), zsh = (uint32_t)__builtin_ctz(2 * bz);
-        const size_t nlive = ((size_t)g.n >> 4) * (g.n >> 4) * (g.n >> zsh);
-        hipError_t e = hipMemsetAsync(g.k3_live, 0, nlive, c->stream);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k3_live_blocks, dim3(1024), dim3(256), 0, c->stream, (const uint32_t*)g.occ_list,
-                           (const uint32_t*)g.occ_count, lgn, zsh, g.k3_live);
-        g.k3_live_bz = bz;
-    }
     g.k3_sparse_ok = k2_level0;
     return hipGetLastError();
 }
