@@ -214,6 +214,7 @@ vct_status vct_create(const vct_config* cfg, vct_ctx** out) {
     }
     if (e == hipSuccess) e = hipMalloc((void**)&g.k3_live, nv / 256 > 0 ? nv / 256 : 1);
     if (e == hipSuccess) e = hipMalloc((void**)&g.k3_live_list, (nv / 1024 + 64) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&g.k2_coarse, 2 * 64 * 64 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&g.occ_list, nv * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc((void**)&g.occ_count, 256);
     if (e == hipSuccess) e = hipMemset(g.occ_count, 0, 256);
@@ -296,6 +297,7 @@ void vct_destroy(vct_ctx* c) {
     if (g.occ_list) (void)hipFree(g.occ_list);
     if (g.k3_live) (void)hipFree(g.k3_live);
     if (g.k3_live_list) (void)hipFree(g.k3_live_list);
+    if (g.k2_coarse) (void)hipFree(g.k2_coarse);
     if (g.b0) (void)hipFree(g.b0);
     if (g.occ) (void)hipFree(g.occ);
     if (g.zmap) (void)hipFree(g.zmap);
@@ -389,6 +391,7 @@ static vct_status voxelize_dev(vct_ctx* c, const void* dv, uint32_t stride, uint
     VCT_HIP(hipMemsetAsync(derr, 0, 4, c->stream), "memset err");
     VCT_HIP(launch_voxelize(c, dv, stride, n_verts, di, n_tri, dm, dk, n_mat, dmap, uv_offset, derr), "voxelize");
     c->grid.k3_live_bz = 0;
+    c->grid.k2_coarse_ok = false;
     VCT_HIP(launch_k3_live(c), "K3 live blocks");   // its count arrives with the error word
     int herr = 0;
     VCT_HIP(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, c->stream), "download err");

@@ -61,6 +61,10 @@ struct Grid {
     uint32_t k3_live_count = 0;              // host copy, read back with K1's error word
     int k3_live_bz = 0;
     bool k3_sparse_ok = false;
+    // K2's coarse occupancy bits (one per brick of (n/64)^3 voxels, 64-bit rows): from K1's
+    // occupancy, so built by the first K2 after each K1 and reused by the next ones
+    uint32_t* k2_coarse = nullptr;           // [2 * 64 * 64]
+    bool k2_coarse_ok = false;
     bool voxelized = false, injected = false, mipped = false;
     bool l0_dense = false;   // level 0 was replaced densely (upload / device copy): K2 must clear it whole
     bool l0_on_peers = false;   // multi-device: the other devices hold this level 0 (vct_build_mips copies it)

@@ -828,13 +828,13 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
     // one lane per occupied / lit voxel (n^3 <= 2^30: 32-bit entries)
     int cs = 0;
     while ((g.n >> cs) > 64) ++cs;
-    const uint32_t cn = g.n >> cs, ncw = 2 * cn * cn;   // 64-bit rows
+    const uint32_t cn = g.n >> cs;                       // coarse bricks per axis (<= 64): 2 cn^2 words
     void* sp = nullptr;
-    hipError_t e = scratch_get(c, 4, 256 + nv * 4 + (size_t)ncw * 4, &sp);
+    hipError_t e = scratch_get(c, 4, 256 + nv * 4, &sp);
     if (e != hipSuccess) return e;
     uint32_t* counts = (uint32_t*)sp;            // [0] lit
     uint32_t* lit = (uint32_t*)((char*)sp + 256);
-    uint32_t* coarse = lit + nv;
+    uint32_t* coarse = g.k2_coarse;              // 64-bit rows, one per (y, z) brick row
     hipStream_t s = c->stream;
     if ((e = hipMemsetAsync(counts, 0, 4, s)) != hipSuccess) return e;
     // level 0 is zero outside the occupied voxels (K1's reset clears what K2 wrote)
@@ -843,8 +843,11 @@ hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, flo
         if ((e = hipMemsetAsync(g.pyr, 0, nv * sizeof(float4), s)) != hipSuccess) return e;
         g.l0_dense = false;
     }
-    hipLaunchKernelGGL(k2_coarse, dim3((64 * cn * cn + 255) / 256), dim3(256), 0, s, g.occ_bits, (int)g.n, cs,
-                       coarse);
+    if (!g.k2_coarse_ok) {                       // the first K2 after K1: the occupancy's coarse bits
+        hipLaunchKernelGGL(k2_coarse, dim3((64 * cn * cn + 255) / 256), dim3(256), 0, s, g.occ_bits, (int)g.n, cs,
+                           coarse);
+        g.k2_coarse_ok = true;
+    }
     const uint32_t blocks = (uint32_t)std::min<size_t>((nv / 64 + 255) / 256 + 1, 4096);
     hipLaunchKernelGGL(k2_shade, dim3(blocks), dim3(256), 0, s, g.occ_list, g.occ_count, g.normal, lx, ly, lz, lit,
                        counts, g.pyr, g.n);
