@@ -631,7 +631,17 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     del level0
     ctx.build_mips()
     k3_ms = timed_queued(ctx.build_mips)
-    r.update({"k2_inject_ms": round(k2_ms, 3), "k3_mips_ms": round(k3_ms, 3), "grid_bcast_ms": round(bcast_ms, 3)})
+    # world 1: level 0 came from K2, so those were relight builds (Grid::k3_live).  With more
+    # ranks the broadcast level 0 is a dense write (full builds); the replicated-K2 frame
+    # (every rank injects itself) gets relight builds: timed here after a local injection
+    # (level 0 equals the broadcast one bit for bit, replicated_k2_equals_bcast)
+    k3_rep_ms = k3_ms
+    if world > 1:
+        ctx.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+        ctx.build_mips()
+        k3_rep_ms = max_over_ranks(torch, dist, dev, [timed_queued(ctx.build_mips)], world)[0]
+    r.update({"k2_inject_ms": round(k2_ms, 3), "k3_mips_ms": round(k3_ms, 3), "grid_bcast_ms": round(bcast_ms, 3),
+              "k3_mips_relight_ms": round(k3_rep_ms, 3)})
     if relight_roofs:
         # world 1: level 0 comes from K2 here, so the timed builds are relight builds; with
         # more ranks it arrived through set_level0_from_device (a dense write: full builds)
@@ -703,9 +713,9 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
         "valid_px": frame_valid, "k4_kernel_ms_avg": k4_avg_ms, "k4_kernel_ms_median": k4_med_ms,
         "k4_kernel_ms_avg_overlapped": sum(k4_ov_ms) / len(k4_ov_ms), "overlap": tracer.overlap,
         "local_texels": local_texels, "local_valid": local_valid, "local_steps": local_steps,
-        "frame_relight_ms": round(min(k2_ms + bcast_ms, k2_rep_ms) + k3_ms + ms_per_step, 3),
+        "frame_relight_ms": round(min(k2_ms + bcast_ms + k3_ms, k2_rep_ms + k3_rep_ms) + ms_per_step, 3),
         "frame_relight_bcast_ms": round(k2_ms + bcast_ms + k3_ms + ms_per_step, 3),
-        "frame_relight_replicated_ms": round(k2_rep_ms + k3_ms + ms_per_step, 3),
+        "frame_relight_replicated_ms": round(k2_rep_ms + k3_rep_ms + ms_per_step, 3),
         "replicated_k2_equals_bcast": k2_rep_match,
         "_gb": gb, "_eye": eye, "_steps_px": steps_px,
     })
@@ -826,7 +836,7 @@ def measure_config(args, torch, dist, rank, world, dev, stream, cfg):
            "k4_form_rank0": form_name(m["k4_form"]), "overlap_tune_rank0": m["overlap_tune"],
            "value_single_launch": round(m["frame_cone_steps"] / m["k4_kernel_ms_avg"] / 1e3, 2) if world == 1 else None,
            "roofline_rank0": roof}
-    for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
+    for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "k3_mips_relight_ms", "grid_bcast_ms", "frame_relight_ms",
                "replicated_k2_equals_bcast", "trace_ms_max_rank", "gather_ms", "allgather_ms"):
         if k_ in m:
             out[k_] = m[k_]
@@ -1048,7 +1058,7 @@ def run(args, world):
         result["frame_overlap"] = "two trace streams" if m["overlap"] else "one stream"
         result["overlap_tune"] = m["overlap_tune"]
         result["k4_form"] = form_name(m["k4_form"])
-        for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "grid_bcast_ms", "frame_relight_ms",
+        for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "k3_mips_relight_ms", "grid_bcast_ms", "frame_relight_ms",
                    "frame_relight_bcast_ms", "frame_relight_replicated_ms", "replicated_k2_equals_bcast",
                    "trace_ms_max_rank", "gather_ms", "allgather_ms", "k1_roofline", "k2_roofline", "k3_roofline"):
             if k_ in m:
