@@ -67,3 +67,27 @@ def test_roofline_from_profile(tmp_path):
     assert got is None and "another library build" in why
     r = bench.roofline(got, why, 1.0, 1000, 10, str(p), key)
     assert r["frac"] is None and r["note"]
+
+
+def test_k3_relight_bytes():
+    """bench.k3_relight_bytes: a relight K3 build reads / writes the first launch's bytes
+    only for blocks (16 x 16 x 8 level-0 voxels at the default depth) holding an occupied
+    voxel; every block live = the full build's algorithmic bytes plus the later launches'
+    read of level 3, none live = only the later launches (level 3 read, levels 4..L
+    written)."""
+    import math
+    import numpy as np
+    sys.path.insert(0, REPO)
+    import bench
+    n = 64
+    L = int(math.log2(n))
+    full = n ** 3 * 16 + sum(6 * (n >> l) ** 3 * 16 for l in range(1, L + 1))
+    rest = 6 * (n >> 3) ** 3 * 16 + sum(6 * (n >> l) ** 3 * 16 for l in range(4, L + 1))
+    occ = np.zeros((n, n, n), np.float32)
+    assert bench.k3_relight_bytes(occ, n) == (rest, 0.0)
+    occ[::8, ::16, ::16] = 1.0                       # one voxel in every block
+    assert bench.k3_relight_bytes(occ, n) == (full + 6 * (n >> 3) ** 3 * 16, 1.0)
+    occ[:] = 0.0
+    occ[0, 0, 0] = occ[n - 1, n - 1, n - 1] = 1.0      # two of (n/16)^2 (n/8) blocks
+    b, frac = bench.k3_relight_bytes(occ, n)
+    assert frac == 2 / ((n // 16) ** 2 * (n // 8)) and rest < b < full
