@@ -647,6 +647,7 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
         # more ranks it arrived through set_level0_from_device (a dense write: full builds)
         r.update(relight_roofline(ctx, n, scene_name, r["k1_voxelize_ms"], k2_ms, k3_ms, k3_sparse=world == 1))
 
+    progress(rank, f"  {scene_name}: K1-K3 timed")
     cam = Camera()
     eye = [float(x) for x in cam.position]
     if args.gbuffer == "scene":
@@ -679,7 +680,9 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     # workload and keeps the faster (vct_trace_form); let that settle before the warmup
     r["k4_form"] = settle_form(ctx, torch, lambda: tracer.trace_local(gb, eye, variant=args.variant))
     # one stream or two (FrameTracer.tune: 16 + 16 timed frames, before the warmup)
+    progress(rank, f"  {scene_name}: counting frame done")
     r["overlap_tune"] = tracer.tune(gb, eye, variant=args.variant) if tracer.auto else None
+    progress(rank, f"  {scene_name}: overlap tuned")
     for _ in range(args.warmup):
         tracer.frame(gb, eye, variant=args.variant)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -695,6 +698,7 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
         dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(torch, dist, dev, [elapsed], world)[0]
+    progress(rank, f"  {scene_name}: {args.steps} timed frames done")
     k4_ov_ms = [a.elapsed_time(b) for a, b in ev]
     # K4 alone (the roofline's launch duration): K frames back to back on the ctx stream,
     # no other work on the GPU -- in the pipelined loop consecutive traces share the chip
