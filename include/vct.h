@@ -196,6 +196,12 @@ vct_status vct_voxelize_textured_device(vct_ctx* ctx, const void* verts, uint32_
 vct_status vct_inject_directional(vct_ctx* ctx, const float dir_to_light[3], const float color[3]);
 
 /* ---- K3 mip build (A.4) --------------------------------------------------- */
+/* A relight build -- level 0 from vct_inject_directional, and the previous build was one
+ * too, with no vct_voxelize* in between -- rebuilds only the blocks that hold geometry
+ * and keeps the K4 empty-space maps (after K2, level 0 is nonzero exactly at the
+ * occupied voxels).  The result is bit-identical to a full build.  Any dense level-0
+ * write (upload_level0, level0_device, set_level0_from_device, the multi-device peer
+ * copy) makes the next build a full one. */
 vct_status vct_build_mips(vct_ctx* ctx);
 
 /* ---- K4 cone trace (A.5, A.6) ------------------------------------------
