@@ -359,6 +359,35 @@ vct_status vct_download_voxels(vct_ctx* ctx, float* albedo_occ4, float* normal4)
  * point), counts [n^3] uint32.  Either pointer may be NULL. */
 vct_status vct_download_accum(vct_ctx* ctx, int64_t* sums6, uint32_t* counts);
 
+/* ---- grid dump / load (SURVEY.md 5 "checkpoint / resume") ----------------------
+ * The reference persists no state.  A dump is <stem>.json (header: grid config, sections,
+ * payload length and sha256) + <stem>.bin (payload, little-endian); the format
+ * ("vct-dump/2") is spelled out in csrc/vct_dumpio.h and is the same for every
+ * implementation of this header.  Sections:
+ *  VCT_DUMP_VOXELS   K1's state: the occupied voxels with their integer sums and counts.
+ *                    A context loaded from it is voxelized: vct_inject_directional (any
+ *                    light), vct_build_mips, vct_trace and vct_composite_device give what
+ *                    they give after the original vct_voxelize, bit for bit.  The
+ *                    triangles are not dumped (the G-buffer passes of a loaded context see
+ *                    an empty mesh).
+ *  VCT_DUMP_LEVEL0   the level-0 radiance (K2's output or an upload); loading it builds
+ *                    the mips, so the context can trace at once.
+ *  VCT_DUMP_PYRAMID  every face of levels 1..L; on load the rebuilt pyramid is checked
+ *                    against it bit for bit (VCT_EINVAL on a difference).
+ * Save needs the state a section comes from (VCT_ESTATE otherwise).  Load first checks
+ * the payload's length and sha256 and that the dump's grid (n, aabb_min, extent, aniso)
+ * is the context's, bit for bit (VCT_EINVAL otherwise, nothing changed); then it
+ * replaces the context's grid state.  Synchronous. */
+#define VCT_DUMP_VOXELS  0x1u
+#define VCT_DUMP_LEVEL0  0x2u
+#define VCT_DUMP_PYRAMID 0x4u
+vct_status vct_save_grid(vct_ctx* ctx, const char* stem, uint32_t what);
+vct_status vct_load_grid(vct_ctx* ctx, const char* stem);
+/* A dump's header only: the config it was saved from (device = -1) and its sections,
+ * to create a matching context (no context needed; VCT_EINVAL for a missing or malformed
+ * header). */
+vct_status vct_dump_info(const char* stem, vct_config* cfg, uint32_t* what);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,7 +44,7 @@ struct vct_ctx {
     uint32_t n_tex;
     int voxelized, injected, mipped;
     int comm;               /* vct_comm_init was called (one rank) */
-    char err[256];
+    char err[1024];
 };
 
 static vct_status fail(vct_ctx* c, vct_status s, const char* msg) {
@@ -673,4 +673,118 @@ vct_status vct_download_accum(vct_ctx* c, int64_t* sums6, uint32_t* counts) {
     if (sums6) memcpy(sums6, c->sums, nv * 6 * sizeof(int64_t));
     if (counts) memcpy(counts, c->counts, nv * sizeof(uint32_t));
     return VCT_OK;
+}
+
+/* ---- grid dump / load: the shared "vct-dump/2" format (csrc/vct_dumpio.c, compiled in
+   here too so that a dump written by one implementation loads into the other) -------- */
+#include "../voxel-based-global-illumination_amd/csrc/vct_dumpio.h"
+
+vct_status vct_dump_info(const char* stem, vct_config* cfg, uint32_t* what) {
+    if (!stem) return VCT_EINVAL;
+    vdump_header h;
+    char err[512];
+    if (vdump_read_header(stem, &h, err, sizeof err)) return VCT_EINVAL;
+    if (cfg) *cfg = h.cfg;
+    if (what) *what = h.what;
+    return VCT_OK;
+}
+
+vct_status vct_save_grid(vct_ctx* c, const char* stem, uint32_t what) {
+    if (!c || !stem) return VCT_EINVAL;
+    if (!what || (what & ~(VCT_DUMP_VOXELS | VCT_DUMP_LEVEL0 | VCT_DUMP_PYRAMID)))
+        return fail(c, VCT_EINVAL, "save_grid: `what` must be a nonzero set of VCT_DUMP_* bits");
+    if ((what & VCT_DUMP_PYRAMID) && !(what & VCT_DUMP_LEVEL0))
+        return fail(c, VCT_EINVAL, "save_grid: VCT_DUMP_PYRAMID needs VCT_DUMP_LEVEL0");
+    if ((what & VCT_DUMP_VOXELS) && !c->voxelized) return fail(c, VCT_ESTATE, "save_grid: no voxelization to dump");
+    if ((what & VCT_DUMP_LEVEL0) && !c->injected) return fail(c, VCT_ESTATE, "save_grid: no level 0 (inject first)");
+    if ((what & VCT_DUMP_PYRAMID) && !c->mipped) return fail(c, VCT_ESTATE, "save_grid: no pyramid (build_mips first)");
+    const size_t nv = (size_t)c->n * c->n * c->n;
+    vdump_header h;
+    memset(&h, 0, sizeof h);
+    h.cfg = c->cfg;
+    h.cfg.device = -1;
+    h.what = what;
+    size_t occ = 0;
+    if (what & VCT_DUMP_VOXELS)
+        for (size_t v = 0; v < nv; ++v) occ += c->counts[v] != 0;
+    h.occupied = occ;
+    vdump_file w;
+    char err[512];
+    if (vdump_open_write(&w, stem, &h, err, sizeof err)) return fail(c, VCT_EINVAL, err);
+    int bad = 0;
+    if (what & VCT_DUMP_VOXELS) {
+        for (size_t v = 0; v < nv && !bad; ++v)
+            if (c->counts[v]) { const uint32_t i = (uint32_t)v; bad = vdump_write(&w, &i, 4, err, sizeof err); }
+        for (size_t v = 0; v < nv && !bad; ++v)
+            if (c->counts[v]) bad = vdump_write(&w, c->sums + 6 * v, 48, err, sizeof err);
+        for (size_t v = 0; v < nv && !bad; ++v)
+            if (c->counts[v]) bad = vdump_write(&w, c->counts + v, 4, err, sizeof err);
+    }
+    if (!bad && (what & VCT_DUMP_LEVEL0)) bad = vdump_write(&w, c->r0, nv * 16, err, sizeof err);
+    if (!bad && (what & VCT_DUMP_PYRAMID))
+        bad = vdump_write(&w, c->pyr, vo_pyramid_floats(c->n, c->aniso) * sizeof(float), err, sizeof err);   /* levels 1..L */
+    if (bad) { vdump_close(&w); return fail(c, VCT_EINVAL, err); }
+    if (vdump_close_write(&w, err, sizeof err)) return fail(c, VCT_EINVAL, err);
+    return VCT_OK;
+}
+
+vct_status vct_load_grid(vct_ctx* c, const char* stem) {
+    if (!c || !stem) return VCT_EINVAL;
+    vdump_file r;
+    char err[1024];
+    if (vdump_open_read(&r, stem, err, sizeof err)) return fail(c, VCT_EINVAL, err);
+    vct_status st = VCT_OK;
+    const vdump_header h = r.h;
+    const size_t nv = (size_t)c->n * c->n * c->n;
+    uint32_t *idx = NULL, *cnt = NULL;
+    int64_t* sums = NULL;
+    float *buf = NULL, *pyr = NULL;
+    if (vdump_check_config(&h, &c->cfg, err, sizeof err)) { st = fail(c, VCT_EINVAL, err); goto done; }
+    if ((h.what & VCT_DUMP_PYRAMID) && !(h.what & VCT_DUMP_LEVEL0)) {
+        st = fail(c, VCT_EINVAL, "load_grid: a pyramid section without level 0");
+        goto done;
+    }
+    if (h.what & VCT_DUMP_VOXELS) {
+        const size_t occ = (size_t)h.occupied;
+        idx = (uint32_t*)malloc(occ * 4 + 4);
+        cnt = (uint32_t*)malloc(occ * 4 + 4);
+        sums = (int64_t*)malloc(occ * 48 + 8);
+        if (!idx || !cnt || !sums) { st = fail(c, VCT_ENOMEM, "load_grid: host memory"); goto done; }
+        if (vdump_read(&r, idx, occ * 4, err, sizeof err) || vdump_read(&r, sums, occ * 48, err, sizeof err) ||
+            vdump_read(&r, cnt, occ * 4, err, sizeof err)) { st = fail(c, VCT_EINVAL, err); goto done; }
+        for (size_t i = 0; i < occ; ++i)
+            if (idx[i] >= nv || (i && idx[i] <= idx[i - 1]) || cnt[i] == 0) {
+                st = fail(c, VCT_EINVAL, "load_grid: voxel section is not ascending in-range occupied voxels");
+                goto done;
+            }
+        memset(c->sums, 0, nv * 6 * sizeof(int64_t));
+        memset(c->counts, 0, nv * sizeof(uint32_t));
+        for (size_t i = 0; i < occ; ++i) {
+            memcpy(c->sums + 6 * (size_t)idx[i], sums + 6 * i, 48);
+            c->counts[idx[i]] = cnt[i];
+        }
+        vo_resolve(c->n, c->sums, c->counts, c->albedo_occ, c->normal);
+        free(c->tri); free(c->uv);
+        c->tri = NULL; c->uv = NULL; c->n_tri = 0;     /* the triangles are not part of a dump */
+        c->voxelized = 1;
+        c->injected = c->mipped = 0;
+    }
+    if (h.what & VCT_DUMP_LEVEL0) {
+        buf = (float*)malloc(nv * 16);
+        if (!buf) { st = fail(c, VCT_ENOMEM, "load_grid: host memory"); goto done; }
+        if (vdump_read(&r, buf, nv * 16, err, sizeof err)) { st = fail(c, VCT_EINVAL, err); goto done; }
+        if ((st = vct_upload_level0(c, buf)) != VCT_OK || (st = vct_build_mips(c)) != VCT_OK) goto done;
+        if (h.what & VCT_DUMP_PYRAMID) {
+            const size_t pf = vo_pyramid_floats(c->n, c->aniso);   /* levels 1..L */
+            pyr = (float*)malloc(pf * sizeof(float) + 4);
+            if (!pyr) { st = fail(c, VCT_ENOMEM, "load_grid: host memory"); goto done; }
+            if (vdump_read(&r, pyr, pf * sizeof(float), err, sizeof err)) { st = fail(c, VCT_EINVAL, err); goto done; }
+            if (memcmp(pyr, c->pyr, pf * sizeof(float)) != 0)
+                st = fail(c, VCT_EINVAL, "load_grid: the rebuilt pyramid differs from the dump");
+        }
+    }
+done:
+    vdump_close(&r);
+    free(idx); free(cnt); free(sums); free(buf); free(pyr);
+    return st;
 }

@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "vct.h"
 
@@ -100,6 +101,56 @@ int main(int argc, char** argv) {
     int64_t* sums = malloc((size_t)n * n * n * 48);
     uint32_t* cnt = malloc((size_t)n * n * n * 4);
     CHECK(vct_download_accum(c, sums, cnt));
+    /* grid dump / load (the shared vct_dumpio.c): a round trip, then damaged headers and
+       payloads, each refused with VCT_EINVAL */
+    {
+        char stem[256], path[300];
+        snprintf(stem, sizeof stem, "%s/vct_san_dump_%d_%u", getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp",
+                 (int)getpid(), n);
+        CHECK(vct_save_grid(c, stem, VCT_DUMP_VOXELS | VCT_DUMP_LEVEL0 | VCT_DUMP_PYRAMID));
+        vct_ctx* c2 = NULL;
+        CHECK(vct_create(&cfg, &c2));
+        CHECK(vct_load_grid(c2, stem));
+        float* l0a = malloc((size_t)n * n * n * 16);
+        float* l0b = malloc((size_t)n * n * n * 16);
+        CHECK(vct_download_level(c, 0, 0, l0a));
+        CHECK(vct_download_level(c2, 0, 0, l0b));
+        if (memcmp(l0a, l0b, (size_t)n * n * n * 16)) { fprintf(stderr, "dump round trip mismatch\n"); return 1; }
+        vct_config got;
+        uint32_t what = 0;
+        CHECK(vct_dump_info(stem, &got, &what));
+        if (got.n != n || what != 7u) { fprintf(stderr, "dump info mismatch\n"); return 1; }
+        snprintf(path, sizeof path, "%s.json", stem);
+        FILE* f = fopen(path, "rb");
+        char hdr[4096];
+        const size_t hl = fread(hdr, 1, sizeof hdr - 1, f);
+        fclose(f);
+        hdr[hl] = 0;
+        static const char* cuts[] = {"\"n\"", "\"aabb_min\"", "\"sha256\"", "[", ":", "\"grid\""};
+        for (size_t k = 0; k < sizeof cuts / sizeof *cuts; ++k) {   /* truncated at each key */
+            const char* at = strstr(hdr, cuts[k]);
+            f = fopen(path, "wb");
+            fwrite(hdr, 1, at ? (size_t)(at - hdr) + 1 : hl / 2, f);
+            fclose(f);
+            EXPECT(vct_load_grid(c2, stem), VCT_EINVAL);
+            EXPECT(vct_dump_info(stem, &got, &what), VCT_EINVAL);
+        }
+        f = fopen(path, "wb");
+        fwrite(hdr, 1, hl, f);
+        fclose(f);
+        snprintf(path, sizeof path, "%s.bin", stem);
+        f = fopen(path, "r+b");
+        fseek(f, 5, SEEK_SET);
+        fputc(0x5a, f);
+        fclose(f);
+        EXPECT(vct_load_grid(c2, stem), VCT_EINVAL);           /* sha256 */
+        remove(path);
+        EXPECT(vct_load_grid(c2, stem), VCT_EINVAL);           /* no payload */
+        snprintf(path, sizeof path, "%s.json", stem);
+        remove(path);
+        vct_destroy(c2);
+        free(l0a); free(l0b);
+    }
     vct_comm_id id;
     CHECK(vct_comm_get_id(&id));
     EXPECT(vct_comm_init(c, &id, 2, 0), VCT_ECOMM);

@@ -125,6 +125,21 @@ hipError_t xchg_leave(vct_ctx* c) {
     c->xchg_stream = c->stream;
     return hipEventRecord(c->xchg_done, c->stream);
 }
+
+void xchg_fail(vct_ctx* c) {
+    // the end event of an exchange that failed part way must still cover what it queued:
+    // on the ctx stream and, for a multi-device context, on every peer stream (a fresh
+    // event per peer; if even that fails, the peer stream is drained)
+    for (vct_ctx* p : c->peers) {
+        if (hipSetDevice(p->device) != hipSuccess || hipEventRecord(p->ev, p->stream) != hipSuccess ||
+            hipSetDevice(c->device) != hipSuccess || hipStreamWaitEvent(c->stream, p->ev, 0) != hipSuccess) {
+            (void)hipSetDevice(p->device);
+            (void)hipStreamSynchronize(p->stream);
+        }
+    }
+    (void)hipSetDevice(c->device);
+    (void)xchg_leave(c);
+}
 }  // namespace vct
 
 extern "C" {
@@ -388,20 +403,30 @@ static vct_status voxelize_dev(vct_ctx* c, const void* dv, uint32_t stride, uint
     }
     m.n_tri = n_tri;
     m.textured = dmap != nullptr;
-    VCT_HIP(hipMemsetAsync(derr, 0, 4, c->stream), "memset err");
-    VCT_HIP(launch_voxelize(c, dv, stride, n_verts, di, n_tri, dm, dk, n_mat, dmap, uv_offset, derr), "voxelize");
-    c->grid.k3_live_bz = 0;
-    c->grid.k2_coarse_ok = false;
-    VCT_HIP(launch_k3_live(c), "K3 live blocks");   // its count arrives with the error word
-    int herr = 0;
-    VCT_HIP(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, c->stream), "download err");
-    VCT_HIP(hipStreamSynchronize(c->stream), "voxelize sync");
-    // a grid from out-of-range indices is partial: inject / mips / trace refuse it (VCT_ESTATE)
-    c->grid.voxelized = herr == 0;
-    c->grid.injected = c->grid.mipped = false;
-    c->grid.k3_sparse_ok = false;            // the occupancy changed: next K3 builds every block
+    // Everything derived from the previous occupancy is invalid from here on, and stays so
+    // if a step below fails part way (K1 has already rewritten the accumulators, the
+    // occupied list and level 0 by then): only the success path sets `voxelized` again
+    Grid& g = c->grid;
+    g.voxelized = g.injected = g.mipped = false;
+    g.k2_coarse_ok = g.k3_sparse_ok = g.zm_valid = false;
+    g.k3_live_bz = 0;
     ++c->grid_epoch;
-    if (herr) return fail(c, VCT_EINVAL, "vertex, material or diffuse-map index out of range");
+    int herr = 0;
+    for (bool packed : {true, false}) {
+        VCT_HIP(hipMemsetAsync(derr, 0, 4, c->stream), "memset err");
+        VCT_HIP(launch_voxelize(c, dv, stride, n_verts, di, n_tri, dm, dk, n_mat, dmap, uv_offset, derr, packed),
+                "voxelize");
+        // the K3 live list of a packed pass is the repeat's too (same occupancy), but it is
+        // queued before the one read-back so that its count arrives with the error word
+        if (packed) VCT_HIP(launch_k3_live(c), "K3 live blocks");
+        VCT_HIP(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, c->stream), "download err");
+        VCT_HIP(hipStreamSynchronize(c->stream), "voxelize sync");
+        // a pass whose packed sums may have overflowed is repeated with the seven-atomic form
+        if ((herr & kK1ErrIndex) || !(herr & kK1ErrRedo)) break;
+    }
+    // a grid from out-of-range indices is partial: inject / mips / trace refuse it (VCT_ESTATE)
+    if (herr & kK1ErrIndex) return fail(c, VCT_EINVAL, "vertex, material or diffuse-map index out of range");
+    g.voxelized = true;
     return VCT_OK;
 }
 
@@ -592,6 +617,7 @@ static vct_status trace_multi(vct_ctx* c, const vct_trace_args* a) {
     void* gp = nullptr;
     void* cp = nullptr;
     VCT_HIP(xchg_enter(c), "stream wait (previous exchange)");
+    XchgScope xs{c};                           // every exit below records the exchange's end
     VCT_HIP(scratch_get(c, 8, world * slice, &gp), "gather buffer");
     if (counting) {
         VCT_HIP(scratch_get(c, 9, world * 16, &cp), "counter buffer");
@@ -640,6 +666,7 @@ static vct_status trace_multi(vct_ctx* c, const vct_trace_args* a) {
     float4* f[2] = {(float4*)a->diffuse4, (float4*)a->spec4};
     VCT_HIP(launch_untile(c, (const float4*)gp, 2, w, h, world, f), "untile");
     VCT_HIP(xchg_leave(c), "event record (exchange end)");
+    xs.done = true;
     return VCT_OK;
 }
 

@@ -240,6 +240,7 @@ vct_status vct_comm_trace_frame(vct_ctx* c, const vct_trace_args* a, int32_t roo
     VCT_HIPC(hipSetDevice(c->device), "hipSetDevice");
     void* gp = nullptr;
     VCT_HIPC(xchg_enter(c), "stream wait (previous exchange)");
+    XchgScope xs{c};                           // every exit below records the exchange's end
     VCT_HIPC(scratch_get(c, 8, L.buffer_tiles * tpx * sizeof(float4) + 256, &gp), "comm gather buffer");
     float4* g = (float4*)gp;
     const uint32_t mine = L.tiles;
@@ -285,6 +286,7 @@ vct_status vct_comm_trace_frame(vct_ctx* c, const vct_trace_args* a, int32_t roo
     }
     if (st != VCT_OK) return st;
     VCT_HIPC(xchg_leave(c), "event record (exchange end)");
+    xs.done = true;
     return VCT_OK;
 }
 

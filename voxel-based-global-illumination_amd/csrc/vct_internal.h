@@ -214,11 +214,20 @@ namespace vct {
 
 // K1
 // d_map (device, n_mat entries, may be NULL): diffuse map of each material in c->tex
-// (-1 none); uv_offset: byte offset of the TexCoords in a vertex record (read when d_map)
+// (-1 none); uv_offset: byte offset of the TexCoords in a vertex record (read when d_map).
+// *d_err (device, zeroed by the caller) collects kK1ErrIndex (an index out of range) and
+// kK1ErrRedo (packed sums may have overflowed: repeat with packed = false); nothing is
+// read back here, so the launch queues without a synchronisation after the candidate count.
+constexpr int kK1ErrIndex = 1, kK1ErrRedo = 2;
 hipError_t launch_voxelize(vct_ctx* c, const void* d_verts,
                            uint32_t stride, uint32_t n_verts, const uint32_t* d_idx, uint32_t n_tri,
                            const uint32_t* d_mat, const float4* d_kd, uint32_t n_mat, const int32_t* d_map,
-                           uint32_t uv_offset, int* d_err);
+                           uint32_t uv_offset, int* d_err, bool packed = true);
+// grid dumps: K1 records [cnt][7] int64 (albedo rgb, normal xyz sums, count) of the voxels
+// d_idx (device) -- read out of the accumulators, or written back into them after the
+// previous voxelization's sparse reset (bits, occupied list and resolved voxels rebuilt)
+hipError_t launch_k1_gather(vct_ctx* c, const uint32_t* d_idx, uint32_t cnt, long long* d_rec);
+hipError_t launch_k1_restore(vct_ctx* c, const uint32_t* d_idx, uint32_t cnt, const long long* d_rec);
 // K2
 hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb);
 // K3 (and the K4 empty-space maps of Grid::zmap)
@@ -265,5 +274,13 @@ hipError_t k4_scratch(vct_ctx* c, int i, size_t bytes, void** out, bool* fresh);
 // and mark its end (vct_ctx::xchg_done)
 hipError_t xchg_enter(vct_ctx* c);
 hipError_t xchg_leave(vct_ctx* c);
+// an exchange that fails after xchg_enter: record its end anyway, covering the work it
+// queued on the ctx stream and the peer streams (XchgScope calls it on every early exit)
+void xchg_fail(vct_ctx* c);
+struct XchgScope {
+    vct_ctx* c;
+    bool done = false;                        // set once xchg_leave has succeeded
+    ~XchgScope() { if (!done) xchg_fail(c); }
+};
 
 }  // namespace vct

@@ -533,13 +533,23 @@ __global__ void __launch_bounds__(256) k3_live_compact(const uint8_t* __restrict
 // 512^3, and 8 x 8 x 2 by 3-4 %: twice the workgroups in flight per CU hide the staging
 // loads better than the one saved launch (relight builds too: tools/k3_shapes.sh).
 // VCT_K3_BZ = 8 | 2 selects the others (A/B).
+// The K3 A/B switches (VCT_K3_BZ, VCT_K3_PLAN, VCT_K3_WRITE, VCT_K3_SPARSE, VCT_ZMAP) are
+// all read per call, so a process can flip one between builds and see exactly that one
+// change (a getenv per build is nothing beside the build).  They interact in one place:
+// VCT_ZMAP=0 leaves the K4 maps invalid, and a relight-sparse build needs the maps of the
+// previous build, so it also turns the sparse builds off.
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+static bool env_off(const char* name) {
+    const char* v = getenv(name);
+    return v && strcmp(v, "0") == 0;
+}
+
 static int k3_block_depth() {
-    static const int bz = [] {
-        const char* v = getenv("VCT_K3_BZ");
-        const int b = v ? atoi(v) : 4;
-        return b == 8 || b == 2 ? b : 4;
-    }();
-    return bz;
+    const int b = env_int("VCT_K3_BZ", 4);
+    return b == 8 || b == 2 ? b : 4;
 }
 
 hipError_t launch_k3_live(vct_ctx* c) {
@@ -567,8 +577,9 @@ hipError_t launch_mips(vct_ctx* c) {
     Grid& g = c->grid;
     const bool zm_was_valid = g.zm_valid;
     g.zm_valid = false;
-    const char* plan = getenv("VCT_K3_PLAN");
-    if (plan && strcmp(plan, "level") == 0) {    // A/B: one lane-per-parent launch per level (no K4 maps)
+    const char* plan = getenv("VCT_K3_PLAN");   // A/B switches: read per call (k3_block_depth)
+    const bool zmap_on = !env_off("VCT_ZMAP");
+    if (plan && strcmp(plan, "level") == 0) {                            // A/B: one lane-per-parent launch per level (no K4 maps)
         for (uint32_t l = 1; l <= g.L; ++l) {
             const int nl = (int)(g.n >> l);
             const size_t vl = (size_t)nl * nl * nl;
@@ -589,17 +600,13 @@ hipError_t launch_mips(vct_ctx* c) {
     // level l of a full 8^3 block goes out in brick order from LDS: whole 512-B runs per
     // wave instead of 64-B half bricks (256^3: 0.126 -> 0.122 ms, 512^3: 0.890 -> 0.857 ms);
     // VCT_K3_WRITE=0 writes each parent from its thread (A/B)
-    static const int bw = [] {
-        const char* v = getenv("VCT_K3_WRITE");
-        return v ? atoi(v) : 1;
-    }();
-    k.brick_writes = bw;
+    k.brick_writes = env_int("VCT_K3_WRITE", 1);
     k.b0 = nullptr;
     const int bz = k3_block_depth();
     // Relight build (Grid::k3_live): level 0 from K2 (not a dense write) and the last build
     // was one too, for this occupancy -- the non-live blocks of the first launch and the K4
     // maps (built from the same nonzero pattern) are skipped.  VCT_K3_SPARSE=0: A/B without.
-    static const bool sparse_on = !(getenv("VCT_K3_SPARSE") && strcmp(getenv("VCT_K3_SPARSE"), "0") == 0);
+    const bool sparse_on = !env_off("VCT_K3_SPARSE");
     const bool k2_level0 = !g.l0_dense;
     const bool sparse = sparse_on && k2_level0 && g.k3_sparse_ok && g.k3_live_bz == bz && g.n >= 16 && zm_was_valid;
     bool built = false;
@@ -633,7 +640,7 @@ hipError_t launch_mips(vct_ctx* c) {
         l += (uint32_t)__builtin_ctz(Ez) + 1u;
     }
     if (built) {
-        g.zm_valid = !(getenv("VCT_ZMAP") && strcmp(getenv("VCT_ZMAP"), "0") == 0);   // VCT_ZMAP=0: A/B without
+        g.zm_valid = zmap_on;                  // VCT_ZMAP=0: A/B without (and without sparse builds)
     }
     if (sparse) g.zm_valid = true;            // same level-0 pattern as when they were built
     g.k3_sparse_ok = k2_level0;

@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(256) k1_tri_setup(
     const int32_t tex = (map && m < n_mat) ? map[m] : -1;
     if (vi[0] >= n_verts || vi[1] >= n_verts || vi[2] >= n_verts || (kd && m >= n_mat) || (map && m >= n_mat) ||
         tex < -1 || (tex >= 0 && (uint32_t)tex >= n_tex)) {
-        atomicOr(err, 1);
+        atomicOr(err, kK1ErrIndex);
         g.ext[0] = g.ext[1] = g.ext[2] = 0;
         counts[t] = 0;
         geom[t] = g;
@@ -372,8 +372,8 @@ __host__ __device__ __forceinline__ void unpack_sums(long long w, long long& lo,
 
 // K1 resolve: accumulators -> albedo/occupancy, normal of the voxels K1 hit (the
 // occupied list k2_list builds from their bits; the other voxels stay zero).  PACKED: a
-// voxel whose count x max|value| could reach 2^31 raises *overflow instead (the host then
-// repeats the voxelization unpacked)
+// voxel whose count x max|value| could reach 2^31 ORs kK1ErrRedo into *overflow (the pass's
+// error word) instead; the host then repeats the voxelization unpacked
 template <bool PACKED>
 __device__ __forceinline__ void resolve_voxel(const long long* __restrict__ accum, size_t v,
                                               float4* __restrict__ albedo_occ, float4* __restrict__ normal,
@@ -401,7 +401,7 @@ __device__ __forceinline__ void resolve_voxel(const long long* __restrict__ accu
         if constexpr (PACKED) {
             s[6] = p1.y;
             if ((unsigned long long)s[6] * maxabs >= (1ull << 31)) {
-                atomicOr(overflow, 1);
+                atomicOr(overflow, kK1ErrRedo);
                 return;
             }
             unpack_sums(p0.x, s[0], s[1]);
@@ -688,18 +688,18 @@ __global__ void __launch_bounds__(256) k2_inject(const float4* __restrict__ albe
     *dst = out;
 }
 
-// One voxelization pass.  packed: try the packed accumulators (k1_candidates); when
-// their exactness bound cannot be shown on the host (more triangles than 2^31 / max|value|)
-// the pass reads back k1_resolve's overflow flag and sets *redo if it fired.
+// One voxelization pass.  packed: try the packed accumulators (k1_candidates); a voxel
+// whose packed sums could have overflowed makes k1_resolve OR kK1ErrRedo into the pass's
+// error word, which the caller reads back with the index-range flag (no extra
+// synchronisation) and then repeats the pass unpacked.
 hipError_t voxelize_pass(vct_ctx* c, const void* d_verts, uint32_t stride, uint32_t n_verts, const uint32_t* d_idx,
                          uint32_t n_tri, const uint32_t* d_mat, const float4* d_kd, uint32_t n_mat,
-                         const int32_t* d_map, uint32_t uv_offset, int* d_err, bool packed, bool* redo) {
+                         const int32_t* d_map, uint32_t uv_offset, int* d_err, bool packed) {
     Grid& g = c->grid;
-    *redo = false;
     hipStream_t s = c->stream;
     const size_t nv = (size_t)g.n * g.n * g.n;
     hipError_t e;
-    // scratch layout: geom | fix | counts | offsets | tile sums | total, max|value|, overflow |
+    // scratch layout: geom | fix | counts | offsets | tile sums | total, max|value| |
     // textured triangles' UVs
     const uint32_t n_tiles = (n_tri + kScanTile - 1) / kScanTile;
     size_t off_geom = 0;
@@ -720,7 +720,6 @@ hipError_t voxelize_pass(vct_ctx* c, const void* d_verts, uint32_t stride, uint3
     unsigned long long* tiles = (unsigned long long*)(base + off_tiles);
     unsigned long long* total = (unsigned long long*)(base + off_total);
     uint32_t* maxabs = (uint32_t*)(base + off_total + 8);
-    int* overflow = (int*)(base + off_total + 12);
     TriUV* tuv = d_map ? (TriUV*)(base + off_uv) : nullptr;
 
     // sparse reset of the previous voxelization (its occupied list), then the bits
@@ -730,8 +729,8 @@ hipError_t voxelize_pass(vct_ctx* c, const void* d_verts, uint32_t stride, uint3
                        g.normal, g.pyr, g.n);
     if ((e = hipMemsetAsync(g.occ_bits, 0, nwords * 8, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(g.occ_count, 0, 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(total, 0, 16, s)) != hipSuccess) return e;   // total, max|value|, overflow
-    bool use_packed = false, check = false;
+    if ((e = hipMemsetAsync(total, 0, 16, s)) != hipSuccess) return e;   // total, max|value|
+    bool use_packed = false;
     if (n_tri > 0) {
         hipLaunchKernelGGL(k1_tri_setup, dim3((n_tri + 255) / 256), dim3(256), 0, s,
                            (const char*)d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat, d_map,
@@ -748,12 +747,11 @@ hipError_t voxelize_pass(vct_ctx* c, const void* d_verts, uint32_t stride, uint3
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
         const unsigned long long h_total = h_head[0];
         const uint32_t h_maxabs = (uint32_t)h_head[1];
-        // a voxel's count never exceeds n_tri: count x max|value| < 2^31 is then certain;
-        // otherwise packed runs with the overflow check (unless a handful of hits could
-        // already overflow: unpacked outright)
+        // a voxel's count never exceeds n_tri: with n_tri x max|value| < 2^31 the resolve's
+        // overflow check can never fire; otherwise it may (then the caller repeats the pass
+        // unpacked).  When a handful of hits could already overflow: unpacked outright
         const unsigned long long safe = h_maxabs ? ((1ull << 31) - 1) / h_maxabs : ~0ull;
         use_packed = packed && safe >= 256;
-        check = use_packed && n_tri > safe;
         if (h_total > 0) {
             unsigned long long threads = (h_total + kCandPerThread - 1) / kCandPerThread;
             unsigned long long blocks = (threads + 255) / 256;
@@ -780,40 +778,94 @@ hipError_t voxelize_pass(vct_ctx* c, const void* d_verts, uint32_t stride, uint3
     g.accum_packed = use_packed;
     if (use_packed)
         hipLaunchKernelGGL(k1_resolve<true>, dim3(lb), dim3(256), 0, s, g.accum, g.occ_list, g.occ_count,
-                           g.albedo_occ, g.normal, maxabs, overflow);
+                           g.albedo_occ, g.normal, maxabs, d_err);
     else
         hipLaunchKernelGGL(k1_resolve<false>, dim3(lb), dim3(256), 0, s, g.accum, g.occ_list, g.occ_count,
-                           g.albedo_occ, g.normal, maxabs, overflow);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (check) {
-        int h_over = 0;
-        if ((e = hipMemcpyAsync(&h_over, overflow, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        *redo = h_over != 0;
-    }
-    return hipSuccess;
+                           g.albedo_occ, g.normal, maxabs, d_err);
+    return hipGetLastError();
 }
 
 }  // namespace
 
-// K1.  Packed accumulators by default (VCT_K1_PACKED=0: the seven-atomic form, for A/B);
-// a pass whose packed sums could have overflowed is repeated unpacked (its occupied list
-// drives the repeat's sparse reset), so the result is the same either way.
+// K1.  Packed accumulators by default (VCT_K1_PACKED=0, read once: the seven-atomic form,
+// for A/B).  packed = false forces the seven-atomic form: the caller's repeat of a pass whose
+// error word came back with kK1ErrRedo (its occupied list drives the repeat's sparse reset),
+// so the result is the same either way.
 hipError_t launch_voxelize(vct_ctx* c, const void* d_verts, uint32_t stride,
                            uint32_t n_verts, const uint32_t* d_idx, uint32_t n_tri, const uint32_t* d_mat,
                            const float4* d_kd, uint32_t n_mat, const int32_t* d_map, uint32_t uv_offset,
-                           int* d_err) {
-    static const bool packed = [] {
+                           int* d_err, bool packed) {
+    static const bool packed_env = [] {
         const char* v = getenv("VCT_K1_PACKED");
         return !(v && strcmp(v, "0") == 0);
     }();
-    bool redo = false;
-    hipError_t e = voxelize_pass(c, d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat, d_map, uv_offset,
-                                 d_err, packed, &redo);
-    if (e == hipSuccess && redo)
-        e = voxelize_pass(c, d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat, d_map, uv_offset, d_err,
-                          false, &redo);
-    return e;
+    return voxelize_pass(c, d_verts, stride, n_verts, d_idx, n_tri, d_mat, d_kd, n_mat, d_map, uv_offset, d_err,
+                         packed && packed_env);
+}
+
+namespace {
+// Grid dumps (vct_save_grid / vct_load_grid): K1's state is the occupied voxels' integer
+// sums and counts.  k1_gather reads them (unpacking a packed record) as [i][7] int64:
+// albedo rgb, normal xyz, count; k1_restore writes such records back into the (cleared)
+// seven-atomic layout and sets the voxels' occupancy bits.
+__global__ void __launch_bounds__(256) k1_gather(const uint32_t* __restrict__ idx, uint32_t cnt,
+                                                 const long long* __restrict__ accum, int packed,
+                                                 long long* __restrict__ out) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
+        const longlong2* a = (const longlong2*)(accum + 8 * (size_t)idx[i]);
+        const longlong2 p0 = a[0], p1 = a[1], p2 = a[2], p3 = a[3];
+        long long s[7];
+        if (packed) {
+            unpack_sums(p0.x, s[0], s[1]);
+            unpack_sums(p0.y, s[2], s[3]);
+            unpack_sums(p1.x, s[4], s[5]);
+            s[6] = p1.y;
+        } else {
+            s[0] = p0.x; s[1] = p0.y; s[2] = p1.x; s[3] = p1.y; s[4] = p2.x; s[5] = p2.y; s[6] = p3.x;
+        }
+        for (int j = 0; j < 7; ++j) out[7 * (size_t)i + j] = s[j];
+    }
+}
+
+__global__ void __launch_bounds__(256) k1_restore(const uint32_t* __restrict__ idx, uint32_t cnt,
+                                                  const long long* __restrict__ rec, long long* __restrict__ accum,
+                                                  unsigned long long* __restrict__ bits) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
+        const size_t v = idx[i];
+        long long* a = accum + 8 * v;
+        for (int j = 0; j < 7; ++j) a[j] = rec[7 * (size_t)i + j];
+        atomicOr(bits + (v >> 6), 1ull << (v & 63));
+    }
+}
+}  // namespace
+
+hipError_t launch_k1_gather(vct_ctx* c, const uint32_t* d_idx, uint32_t cnt, long long* d_rec) {
+    if (cnt == 0) return hipSuccess;
+    hipLaunchKernelGGL(k1_gather, dim3(std::min<uint32_t>((cnt + 255) / 256, 4096)), dim3(256), 0, c->stream, d_idx,
+                       cnt, (const long long*)c->grid.accum, c->grid.accum_packed ? 1 : 0, d_rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_k1_restore(vct_ctx* c, const uint32_t* d_idx, uint32_t cnt, const long long* d_rec) {
+    Grid& g = c->grid;
+    hipStream_t s = c->stream;
+    const size_t nv = (size_t)g.n * g.n * g.n, nwords = nv / 64;
+    const uint32_t lb = (uint32_t)std::min<size_t>((nv + 255) / 256, 4096);
+    // the previous voxelization's sparse reset, as a K1 pass starts (voxelize_pass)
+    hipLaunchKernelGGL(k1_clear, dim3(lb), dim3(256), 0, s, g.occ_list, g.occ_count, g.accum, g.albedo_occ,
+                       g.normal, g.pyr, g.n);
+    hipError_t e;
+    if ((e = hipMemsetAsync(g.occ_bits, 0, nwords * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(g.occ_count, 0, 4, s)) != hipSuccess) return e;
+    if (cnt)
+        hipLaunchKernelGGL(k1_restore, dim3(std::min<uint32_t>((cnt + 255) / 256, 4096)), dim3(256), 0, s, d_idx,
+                           cnt, d_rec, g.accum, g.occ_bits);
+    hipLaunchKernelGGL(k2_list, dim3((uint32_t)((nwords + 255) / 256)), dim3(256), 0, s, g.occ_bits, nwords,
+                       g.occ_list, g.occ_count);
+    g.accum_packed = false;
+    hipLaunchKernelGGL(k1_resolve<false>, dim3(lb), dim3(256), 0, s, g.accum, g.occ_list, g.occ_count,
+                       g.albedo_occ, g.normal, (const uint32_t*)nullptr, (int*)nullptr);
+    return hipGetLastError();
 }
 
 hipError_t launch_inject(vct_ctx* c, float lx, float ly, float lz, float cr, float cg, float cb) {

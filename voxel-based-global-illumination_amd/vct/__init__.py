@@ -23,6 +23,7 @@ device memory, streams and torch.distributed).
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -426,6 +427,15 @@ class Context:
         nm = np.empty((n, n, n, 4), np.float32)
         self._check(self.lib.vct_download_voxels(self.h, _fptr(ao), _fptr(nm)), "download_voxels")
         return ao, nm
+
+    # -- grid dump / load (vct_save_grid / vct_load_grid; vct.dump wraps them) --------
+    def save_grid(self, stem, what: int):
+        """vct_save_grid: what = VCT_DUMP_* bits (vct.dump.VOXELS | LEVEL0 | PYRAMID)."""
+        self._check(self.lib.vct_save_grid(self.h, os.fsencode(str(stem)), what), "save_grid")
+
+    def load_grid(self, stem):
+        """vct_load_grid: replaces this context's grid state with the dump's."""
+        self._check(self.lib.vct_load_grid(self.h, os.fsencode(str(stem))), "load_grid")
 
     def download_accum(self):
         n = self.n

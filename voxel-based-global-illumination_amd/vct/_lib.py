@@ -26,6 +26,7 @@ EXPORTS = (
     "vct_num_levels", "vct_level_dims", "vct_download_level", "vct_upload_level0",
     "vct_level0_device", "vct_copy_level0_to_device", "vct_set_level0_from_device",
     "vct_download_voxels", "vct_download_accum", "vct_device_alloc", "vct_device_free", "vct_memcpy",
+    "vct_save_grid", "vct_load_grid", "vct_dump_info",
 )
 
 STATUS = {0: "VCT_OK", 1: "VCT_EINVAL", 2: "VCT_ENOMEM", 3: "VCT_EDEVICE", 4: "VCT_ECOMM", 5: "VCT_ESTATE"}
@@ -163,6 +164,9 @@ def bind(lib: C.CDLL) -> C.CDLL:
         "vct_device_alloc": (i32, [P, C.c_size_t, C.POINTER(P)]),
         "vct_device_free": (i32, [P, P]),
         "vct_memcpy": (i32, [P, P, P, C.c_size_t, C.c_int]),
+        "vct_save_grid": (i32, [P, C.c_char_p, u32]),
+        "vct_load_grid": (i32, [P, C.c_char_p]),
+        "vct_dump_info": (i32, [C.c_char_p, C.POINTER(VctConfig), C.POINTER(u32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

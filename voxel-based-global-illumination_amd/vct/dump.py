@@ -1,32 +1,41 @@
-"""Grid and G-buffer dump / load: raw ``.bin`` + JSON header (SURVEY.md §5 "checkpoint /
-resume": golden fixtures and repro cases; the reference persists no state).
+"""Grid and G-buffer dump / load (SURVEY.md §5 "checkpoint / resume": golden fixtures,
+repro cases, relighting a saved scene; the reference persists no state).
 
-A dump is two files: ``<stem>.json`` (what the data is) and ``<stem>.bin`` (little-endian
-float32, C order).
+* **Grid** (:func:`save_grid` / :func:`load_grid`) is the C-ABI's ``vct_save_grid`` /
+  ``vct_load_grid`` (``include/vct.h``), so the C++ host and Python write the same files
+  (format ``vct-dump/2``, spelled out in ``csrc/vct_dumpio.h``): ``<stem>.json`` (grid
+  config, sections, payload length and sha256) + ``<stem>.bin``. Sections:
 
-* **Grid** (:func:`save_grid` / :func:`load_grid`). The header holds the context config
-  (n, aabb_min, extent, aniso, cone set) and the byte length and sha256 of the payload.
-  The payload is level 0 as [z][y][x][rgba], the linear layout of ``vct_download_level``
-  and ``vct_upload_level0``. With ``pyramid=True`` it also holds every face of levels
-  1..L, in level-major then face-major order.
-  - Loading uploads level 0 and runs ``vct_build_mips``, which is deterministic.
-  - The rebuilt pyramid is therefore bit-identical to the dumped one. When the dump
-    carries the pyramid, ``verify=True`` checks that.
-* **G-buffer** (:func:`save_gbuffer` / :func:`load_gbuffer`). ``pos4`` / ``nrm4`` /
-  ``alb4`` are [h][w][4] float32 (vct_trace_args), plus the eye position.
+  - ``VOXELS``: K1's state, the occupied voxels' integer sums and counts. A context loaded
+    from it is voxelized: any light can be injected, the mips built, frames traced and
+    composited, bit for bit as after the original ``vct_voxelize`` (the triangles are not
+    dumped);
+  - ``LEVEL0``: the level-0 radiance; loading it builds the mips at once;
+  - ``PYRAMID``: every face of levels 1..L; the rebuilt pyramid is checked against it bit
+    for bit on load.
 
-The payload is checked against the header's length and sha256 before anything is
-uploaded. A truncated or edited dump raises ``ValueError``.
+  Loading checks the payload's length and sha256 and that the dump's grid (n, aabb_min,
+  extent, aniso) is the context's before anything changes; a mismatch or a damaged dump
+  raises ``ValueError``.
+* **G-buffer** (:func:`save_gbuffer` / :func:`load_gbuffer`, Python only: the planes are the
+  host's own data). ``pos4`` / ``nrm4`` / ``alb4`` are [h][w][4] float32 (vct_trace_args),
+  plus the eye position; ``<stem>.json`` + ``<stem>.bin`` (format ``vct-dump/1``, kind
+  ``gbuffer``), the payload checked against the header's length and sha256.
 """
 from __future__ import annotations
 
+import ctypes as C
 import hashlib
 import json
 import os
 
 import numpy as np
 
-FORMAT = "vct-dump/1"
+from . import _lib
+
+VOXELS, LEVEL0, PYRAMID = 0x1, 0x2, 0x4   # VCT_DUMP_*
+GBUF_FORMAT = "vct-dump/1"
+_EINVAL = 1
 
 
 def _paths(stem: str):
@@ -34,6 +43,40 @@ def _paths(stem: str):
     if stem.endswith(".json") or stem.endswith(".bin"):
         stem = stem.rsplit(".", 1)[0]
     return stem + ".json", stem + ".bin"
+
+
+def dump_info(stem, lib=None):
+    """(vct_config fields as a dict, what) of a grid dump's header (vct_dump_info)."""
+    lib = lib if lib is not None else _lib.load()
+    cfg, what = _lib.VctConfig(), C.c_uint32()
+    if lib.vct_dump_info(os.fsencode(_paths(stem)[0]), C.byref(cfg), C.byref(what)) != 0:
+        raise ValueError(f"{_paths(stem)[0]}: not a readable vct-dump/2 grid header")
+    return {"n": cfg.n, "aabb_min": tuple(cfg.aabb_min), "extent": cfg.extent, "aniso": bool(cfg.aniso),
+            "n_diffuse": cfg.n_diffuse, "specular": bool(cfg.specular)}, what.value
+
+
+def save_grid(ctx, stem, pyramid: bool = False, voxels: bool = True, level0: bool = True) -> None:
+    """Dump ctx's K1 state (voxels), level 0 and, pyramid=True, every face of levels 1..L."""
+    what = (VOXELS if voxels else 0) | (LEVEL0 if level0 else 0) | (PYRAMID if pyramid else 0)
+    ctx.save_grid(_paths(stem)[0], what)
+
+
+def load_grid(stem, ctx=None, verify: bool = True, **ctx_kw):
+    """A context (new, or ctx of the same grid) holding the dumped state.  A dumped pyramid
+    is always verified against the rebuilt one (verify is kept for callers' clarity)."""
+    from . import Context, VctError
+    del verify
+    info, _ = dump_info(stem, lib=ctx.lib if ctx is not None else ctx_kw.get("lib"))
+    if ctx is None:
+        ctx = Context(info["n"], info["aabb_min"], info["extent"], aniso=info["aniso"],
+                      n_diffuse=info["n_diffuse"], specular=info["specular"], **ctx_kw)
+    try:
+        ctx.load_grid(_paths(stem)[0])
+    except VctError as e:
+        if e.status == _EINVAL:
+            raise ValueError(str(e)) from None
+        raise
+    return ctx
 
 
 def _write(stem: str, header: dict, arrays) -> None:
@@ -46,7 +89,7 @@ def _write(stem: str, header: dict, arrays) -> None:
             h.update(b)
             size += len(b)
             f.write(b)
-    header = dict(header, format=FORMAT, payload=os.path.basename(bpath), bytes=size, sha256=h.hexdigest())
+    header = dict(header, format=GBUF_FORMAT, payload=os.path.basename(bpath), bytes=size, sha256=h.hexdigest())
     with open(jpath, "w") as f:
         json.dump(header, f, indent=1, sort_keys=True)
 
@@ -55,8 +98,8 @@ def _read(stem: str, kind: str):
     jpath, bpath = _paths(stem)
     with open(jpath) as f:
         header = json.load(f)
-    if header.get("format") != FORMAT or header.get("kind") != kind:
-        raise ValueError(f"{jpath}: not a {FORMAT} {kind} dump")
+    if header.get("format") != GBUF_FORMAT or header.get("kind") != kind:
+        raise ValueError(f"{jpath}: not a {GBUF_FORMAT} {kind} dump")
     with open(bpath, "rb") as f:
         raw = f.read()
     if len(raw) != header["bytes"] or hashlib.sha256(raw).hexdigest() != header["sha256"]:
@@ -64,50 +107,7 @@ def _read(stem: str, kind: str):
     return header, np.frombuffer(raw, dtype="<f4")
 
 
-def save_grid(ctx, stem: str, pyramid: bool = False) -> None:
-    """Dump ctx's level 0 (and, pyramid=True, every face of levels 1..L)."""
-    arrays = [ctx.download_level(0)]
-    levels = []
-    for l in range(ctx.num_levels):
-        nl, nf = ctx.level_dims(l)
-        levels.append({"level": l, "n": int(nl), "faces": int(nf)})
-        if pyramid and l > 0:
-            arrays += [ctx.download_level(l, f) for f in range(nf)]
-    header = {"kind": "grid", "n": ctx.n, "aabb_min": list(ctx.aabb_min), "extent": ctx.extent,
-              "aniso": bool(ctx.aniso), "n_diffuse": ctx.n_diffuse, "specular": bool(ctx.specular),
-              "levels": levels, "pyramid": bool(pyramid)}
-    _write(stem, header, arrays)
-
-
-def load_grid(stem: str, ctx=None, verify: bool = True, **ctx_kw):
-    """Context (new, or ctx with the same n / aniso) holding the dumped grid: level 0
-    uploaded, mips rebuilt; with a dumped pyramid and verify, checked bit for bit."""
-    from . import Context
-    header, data = _read(stem, "grid")
-    n = int(header["n"])
-    if ctx is None:
-        ctx = Context(n, header["aabb_min"], header["extent"], aniso=header["aniso"],
-                      n_diffuse=header["n_diffuse"], specular=header["specular"], **ctx_kw)
-    elif ctx.n != n or bool(ctx.aniso) != bool(header["aniso"]):
-        raise ValueError(f"dump is n={n} aniso={header['aniso']}, context n={ctx.n} aniso={ctx.aniso}")
-    nv = n ** 3 * 4
-    if data.size < nv:
-        raise ValueError("payload shorter than level 0")
-    ctx.upload_level0(data[:nv].reshape(n, n, n, 4))
-    ctx.build_mips()
-    if header["pyramid"] and verify:
-        off = nv
-        for lv in header["levels"][1:]:
-            cnt = lv["n"] ** 3 * 4
-            for f in range(lv["faces"]):
-                want = data[off:off + cnt].reshape(lv["n"], lv["n"], lv["n"], 4)
-                if not np.array_equal(ctx.download_level(lv["level"], f), want):
-                    raise ValueError(f"rebuilt level {lv['level']} face {f} differs from the dump")
-                off += cnt
-    return ctx
-
-
-def save_gbuffer(stem: str, pos4: np.ndarray, nrm4: np.ndarray, alb4: np.ndarray, eye) -> None:
+def save_gbuffer(stem, pos4: np.ndarray, nrm4: np.ndarray, alb4: np.ndarray, eye) -> None:
     h, w = pos4.shape[:2]
     for a in (pos4, nrm4, alb4):
         if a.shape != (h, w, 4):
@@ -116,7 +116,7 @@ def save_gbuffer(stem: str, pos4: np.ndarray, nrm4: np.ndarray, alb4: np.ndarray
            [pos4, nrm4, alb4])
 
 
-def load_gbuffer(stem: str):
+def load_gbuffer(stem):
     """-> (pos4, nrm4, alb4, eye) as [h][w][4] float32 arrays and a 3-tuple"""
     header, data = _read(stem, "gbuffer")
     w, h = int(header["width"]), int(header["height"])
