@@ -397,7 +397,7 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
     # bits 20-23: diffuse parts of the split (3, 4 -> 3 parts of 3 cones, 5, 9 -> one cone each)
     for variant in (0, 1, 0x100, 0x200, 0x400, 0x800, 0x400, 0x300400, 0x400400, 0x500400, 0x900400, 0x900400,
                     0x500400, 0, 0x8000, 0x8400, 0x8800, 0x8200, 0x8000, 0x1000000, 0x2000000, 0x2000400,
-                    0x2000800, 0x2008000, 0x4000000, 0x6000000, 0):
+                    0x2000800, 0x2008000, 0x4000000, 0x6000000, 0x2400, 0x902400, 0x502400, 0x2002400, 0):
         d = torch.full((h, w, 4), -1.0, device=dev)
         sp = torch.full((h, w, 4), -1.0, device=dev)
         cnt = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -408,7 +408,7 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         assert int(cnt[0]) == ref["cone_steps"]
     # no counters at all: the form compiled without the counting instructions (the
     # bench's timed launches), and 0x4000 = the counting form without counters
-    for variant in (0, 0x4000, 0x400, 0x800, 0x200, 0x500400, 0x300400, 0):
+    for variant in (0, 0x4000, 0x400, 0x800, 0x200, 0x500400, 0x300400, 0x902400, 0):
         d = torch.full((h, w, 4), -1.0, device=dev)
         sp = torch.full((h, w, 4), -1.0, device=dev)
         ctx.trace_device(*gb, w, h, cam.position, d, sp, variant=variant)
@@ -417,7 +417,7 @@ def test_trace_variants_bitexact(gpu_ready, oracle_mod, kind):
         assert np.array_equal(sp.cpu().numpy(), ref["spec"]), f"variant {variant:#x} spec (no counters)"
     # variants retired in round 4 (vct_variants.h) are refused, not silently remapped
     from vct import VctError
-    for variant in (2, 3, 0x1000, 0x2000, 0x8002):
+    for variant in (2, 3, 0x1000, 0x8002):
         with pytest.raises(VctError):
             ctx.trace_device(*gb, w, h, cam.position, d, sp, variant=variant)
     ctx.close()

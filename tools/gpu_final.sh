@@ -15,12 +15,12 @@ rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/trace.stderr; exit
 # keep the summaries (the full per-dispatch trace of a whole bench run exceeds what gpurun copies back)
 find $OUT/trace -name "*kernel_stats.csv" -exec cp {} $OUT/ \;
 python3 - $OUT <<'PY'
-import csv, glob, json, sys
+import csv, glob, json, re, sys
 out = sys.argv[1]
 f = glob.glob(out + "/trace/**/*kernel_trace.csv", recursive=True)[0]
 d = {}
 for r in csv.DictReader(open(f)):
-    if "k4_trace" in r["Kernel_Name"] and r["Kernel_Name"].rstrip().endswith("false>(vct::(anonymous namespace)::TraceK)"):
+    if re.search(r"k4_trace<[^>]*, false(?:, \d+)?>\(", r["Kernel_Name"]):   # the counter-free (timed) form
         d.setdefault(r["Kernel_Name"] + " grid " + r["Grid_Size_X"], []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 json.dump({k: {"dispatches": len(v), "avg_ms": sum(v) / len(v) / 1e6} for k, v in d.items()}, open(out + "/k4_timed_dispatches.json", "w"), indent=1)
 PY

@@ -21,7 +21,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-TIMED = re.compile(r"k4_trace<[^>]*, false>\(")
+TIMED = re.compile(r"k4_trace<[^>]*, false(?:, \d+)?>\(")   # the counter-free form (any waves per workgroup)
 
 
 def per_kernel(d):

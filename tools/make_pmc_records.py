@@ -29,7 +29,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-TIMED = re.compile(r"k4_trace<[^>]*, false>\(")
+TIMED = re.compile(r"k4_trace<[^>]*, false(?:, \d+)?>\(")   # the counter-free form (any waves per workgroup)
 # kernels of each relight call (vct_voxelize.hip, vct_mips.hip); k2_list builds K1's occupied list
 STAGES = {
     "k1": re.compile(r"^(?:void )?(?:vct::\(anonymous namespace\)::)?(k1_\w+|k_scan_\w+|k2_list)\b"),

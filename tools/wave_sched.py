@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--variant", type=lambda x: int(x, 0), default=0)
     ap.add_argument("--slots", type=int, default=256 * 16)
     ap.add_argument("--wv", action="store_true", help="timeline-only build (make wv), no phase clocks")
+    ap.add_argument("--world", type=int, default=1, help="trace rank --rank's tiles of a --world split")
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--parts", type=int, default=0, help="cone parts of the launch (per-part wave stats)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -61,10 +64,17 @@ def main():
     cam = Camera()
     gb = [torch.empty((a.h, a.w, 4), device=dev) for _ in range(3)]
     ctx.gbuffer_raster_device(cam, a.w, a.h, scenes.ROUGHNESS, *gb)
-    d = torch.empty((a.h, a.w, 4), device=dev)
-    sp = torch.empty((a.h, a.w, 4), device=dev)
-    for _ in range(2):
-        ctx.trace_device(*gb, a.w, a.h, cam.position, d, sp, variant=a.variant)
+    from vct.multi import tiles_for_rank
+    opx = tiles_for_rank(a.w, a.h, a.rank, a.world) * 4096 if a.world > 1 else a.w * a.h
+    d = torch.empty((opx, 4), device=dev)
+    sp = torch.empty((opx, 4), device=dev)
+    if a.world == 1 and not a.variant & (0x8000 | 0x4000000):
+        # a one-rank frame's tuner alternates screen order and ray reordering while it times
+        # them: their grids differ, so one launch's records would be mixed with the other's
+        a.variant |= 0x4000000
+    for _ in range(64 if a.world > 1 else 2):   # settle the form of this launch, then record the last
+        ctx.trace_device(*gb, a.w, a.h, cam.position, d, sp, variant=a.variant, tile_rank=a.rank,
+                         tile_world=a.world, tile_compact=a.world > 1)
         torch.cuda.synchronize()
     nw = 1 << 18
     buf = np.zeros((nw, 3), np.uint64)
@@ -116,6 +126,15 @@ def main():
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     out["xcd_last_end_us"] = [round(float(en[xcc == x].max()), 1) if (xcc == x).any() else 0.0 for x in range(8)]
     out["xcd_sum_wave_ms"] = [round(float(dur[xcc == x].sum()) / 1e3, 1) for x in range(8)]
+    if a.parts > 1:   # the launch's cone parts (dispatched one after another in blockIdx order)
+        nb = (int(used.max()) + 1) // a.parts
+        part = used // max(nb, 1)
+        out["parts"] = [{"waves": int((part == p).sum()), "mean_us": round(float(dur[part == p].mean()), 1),
+                         "p90_us": round(float(np.percentile(dur[part == p], 90)), 1),
+                         "max_us": round(float(dur[part == p].max()), 1),
+                         "first_start_us": round(float(st[part == p].min()), 1),
+                         "last_end_us": round(float(en[part == p].max()), 1)}
+                        for p in range(a.parts) if (part == p).any()]
     np.save(os.path.join(REPO, "gpurun_out", f"waves_{a.scene}_{a.variant:#x}{'_wv' if a.wv else ''}.npy"),
             buf[:int(used.max()) + 1])
     print(json.dumps(out))

@@ -8,19 +8,35 @@
 // turns into per-lane gathers that miss L2 (HBM-bound at ~91 % of peak with a 2.3x
 // line overfetch).
 //
-// Reordering: a key per pixel = the Morton code of the level-0 voxel holding its cone
-// origin o = (P - g0) / h + n (the same binary32 sequence as K4), background pixels
-// after every valid one; a device radix sort (rocPRIM) of (key, pixel) pairs; K4 then
-// reads lane j of wave w from pixel perm[64 w + j] and writes its outputs back to that
-// pixel.  Cones of one wave start in a few neighbouring voxels, so their footprints
-// share bricks and cache lines.  Every pixel runs exactly the arithmetic it runs
-// without the reordering, so outputs and step counts are bit-identical (tested).
-#include <rocprim/device/device_radix_sort.hpp>
-
+// Reordering: the frame's pixels are grouped by the cell that holds their cone origin
+// o = (P - g0) / h + n (the same binary32 sequence as K4), cells in Morton order,
+// background pixels after every valid one; K4 then reads lane j of wave w from pixel
+// perm[64 w + j] and writes its outputs back to that pixel.  Cones of one wave start in
+// a few neighbouring cells, so their footprints share bricks and cache lines.  Every
+// pixel runs exactly the arithmetic it runs without the reordering, so outputs and step
+// counts are bit-identical whatever the order inside a cell (tested).
+//
+// The grouping is a counting sort, hand-written for the job (round 5; it replaced a
+// rocPRIM radix sort of (Morton code, pixel) pairs, four one-sweep passes):
+//   k_reorder_count    per pixel its cell (Morton code at level lk: at most 2^21 cells,
+//                      level 0 up to 128^3, level 1 at 256^3, level 2 at 512^3) and
+//                      its rank in that cell from an atomic on the cell's counter (the
+//                      background's counter is bumped once per wave: ballot + mbcnt);
+//   k_scan_reduce /    exclusive scan of the counters into cell offsets: tile sums of
+//   k_scan_tiles /     4096 counters, a one-block scan of the tile sums, the tiles'
+//   k_scan_down        own scans with their carries (in place);
+//   k_reorder_scatter  perm[offset(cell) + rank] = pixel.
+// One pass over the pixels, two over the counters (8 MB at most), one scatter: no key
+// bits are sorted twice.  The order inside a cell follows the atomics (it only moves
+// pixels between the waves of that cell, never their results).
 #include "vct_internal.h"
 
 namespace vct {
 namespace {
+
+constexpr uint32_t kMaxCellBits = 21;       // at most 2^21 cells (8 MB of counters)
+constexpr int kScanPer = 16;                // counters per thread in the scan kernels
+constexpr uint32_t kScanTile = 256u * kScanPer;
 
 __device__ __forceinline__ uint32_t spread3(uint32_t v) {   // 10 bits -> every third bit
     v &= 0x3ffu;
@@ -31,27 +47,118 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v) {   // 10 bits -> every 
     return v;
 }
 
-__global__ void __launch_bounds__(256) k_reorder_keys(const float4* __restrict__ pos, const float4* __restrict__ nrm,
-                                                      uint32_t npx, float g0x, float g0y, float g0z, float inv_h,
-                                                      int n, uint32_t* __restrict__ keys,
-                                                      uint32_t* __restrict__ vals) {
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// exclusive prefix sum of one value per thread over a 256-thread block, and the block total
+__device__ __forceinline__ uint32_t block_scan256(uint32_t v, uint32_t& total) {
+    __shared__ uint32_t wt[4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl += t;
+    }
+    if (lane == 63) wt[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += wt[w];
+    total = wt[0] + wt[1] + wt[2] + wt[3];
+    __syncthreads();
+    return before + incl - v;
+}
+
+// cell of each pixel's cone origin (cells = level-lk voxels in Morton order; background =
+// cell ncell) and its rank among the pixels of that cell
+__global__ void __launch_bounds__(256) k_reorder_count(const float4* __restrict__ pos, const float4* __restrict__ nrm,
+                                                       uint32_t npx, float g0x, float g0y, float g0z, float inv_h,
+                                                       int n, int lk, uint32_t ncell, uint32_t* __restrict__ cnt,
+                                                       uint32_t* __restrict__ cell, uint32_t* __restrict__ rank) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= npx) return;
-    const float4 P = pos[i];
-    uint32_t key = 1u << 30;                 // background: after every valid pixel
-    if (P.w != 0.0f) {
+    const bool in = i < npx;
+    float4 P = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (in) P = pos[i];
+    const bool bg = in && P.w == 0.0f;
+    uint32_t c = ncell, r = 0;
+    if (in && !bg) {
         const float4 N = nrm[i];
         const float ox = (P.x - g0x) * inv_h + N.x;   // the cone origin of K4 (level-0 voxel units)
         const float oy = (P.y - g0y) * inv_h + N.y;
         const float oz = (P.z - g0z) * inv_h + N.z;
-        const auto cell = [n](float q) {
-            const float f = floorf(q);
-            return (uint32_t)(f < 0.0f ? 0 : (f > (float)(n - 1) ? n - 1 : (int)f));
+        const auto q = [n, lk](float v) {
+            const float f = floorf(v);
+            return (uint32_t)(f < 0.0f ? 0 : (f > (float)(n - 1) ? n - 1 : (int)f)) >> lk;
         };
-        key = spread3(cell(ox)) | (spread3(cell(oy)) << 1) | (spread3(cell(oz)) << 2);
+        c = spread3(q(ox)) | (spread3(q(oy)) << 1) | (spread3(q(oz)) << 2);
+        r = atomicAdd(cnt + c, 1u);
     }
-    keys[i] = key;
-    vals[i] = i;
+    // the background shares one counter: one atomic per wave
+    const unsigned long long bm = __builtin_amdgcn_ballot_w64(bg);
+    if (bm) {
+        const int lead = __builtin_ctzll(bm);
+        uint32_t base = 0;
+        if ((int)(threadIdx.x & 63) == lead) base = atomicAdd(cnt + ncell, (uint32_t)__builtin_popcountll(bm));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, lead);
+        if (bg) r = base + lanes_below(bm);
+    }
+    if (in) {
+        cell[i] = c;
+        rank[i] = r;
+    }
+}
+
+// counters [t * kScanTile, (t + 1) * kScanTile) -> tile sum t
+__global__ void __launch_bounds__(256) k_scan_reduce(const uint32_t* __restrict__ cnt, uint32_t m,
+                                                     uint32_t* __restrict__ tiles) {
+    const uint32_t base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanPer; ++j) s += base + j < m ? cnt[base + j] : 0u;
+    uint32_t total;
+    (void)block_scan256(s, total);
+    if (threadIdx.x == 0) tiles[blockIdx.x] = total;
+}
+
+// exclusive scan of the tile sums in one block (ntiles <= 2^21 / 4096 + 1 = 513: three rounds)
+__global__ void __launch_bounds__(256) k_scan_tiles(uint32_t* __restrict__ tiles, uint32_t ntiles) {
+    uint32_t carry = 0;
+    for (uint32_t b = 0; b < ntiles; b += 256) {
+        const uint32_t i = b + threadIdx.x;
+        const uint32_t v = i < ntiles ? tiles[i] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_scan256(v, total);
+        if (i < ntiles) tiles[i] = carry + ex;
+        carry += total;
+    }
+}
+
+// in place: counter -> offset of its cell (tile carry + scan inside the tile)
+__global__ void __launch_bounds__(256) k_scan_down(uint32_t* __restrict__ cnt, uint32_t m,
+                                                   const uint32_t* __restrict__ tiles) {
+    const uint32_t base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    uint32_t v[kScanPer], s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanPer; ++j) {
+        v[j] = base + j < m ? cnt[base + j] : 0u;
+        s += v[j];
+    }
+    uint32_t total;
+    uint32_t run = tiles[blockIdx.x] + block_scan256(s, total);
+#pragma unroll
+    for (int j = 0; j < kScanPer; ++j) {
+        if (base + j < m) cnt[base + j] = run;
+        run += v[j];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_reorder_scatter(const uint32_t* __restrict__ cell,
+                                                         const uint32_t* __restrict__ rank,
+                                                         const uint32_t* __restrict__ offs, uint32_t npx,
+                                                         uint32_t* __restrict__ perm) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < npx) perm[offs[cell[i]] + rank[i]] = i;
 }
 
 }  // namespace
@@ -59,27 +166,35 @@ __global__ void __launch_bounds__(256) k_reorder_keys(const float4* __restrict__
 hipError_t launch_reorder(vct_ctx* c, const vct_trace_args* a, const uint32_t** perm) {
     const Grid& g = c->grid;
     const uint32_t npx = a->width * a->height;
-    const size_t pairs = (size_t)npx * sizeof(uint32_t);
-    size_t tmp_bytes = 0;
-    hipError_t e = rocprim::radix_sort_pairs(nullptr, tmp_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, npx, 0, 31, c->stream);
-    if (e != hipSuccess) return e;
-    void* kv = nullptr;   // [keys in | keys out | values in | values out]
-    void* tmp = nullptr;
-    if ((e = k4_scratch(c, kScKeys, 4 * pairs, &kv, nullptr)) != hipSuccess) return e;
-    if ((e = k4_scratch(c, kScSort, tmp_bytes ? tmp_bytes : 1, &tmp, nullptr)) != hipSuccess) return e;
-    uint32_t* keys_in = (uint32_t*)kv;
-    uint32_t* keys_out = keys_in + npx;
-    uint32_t* vals_in = keys_out + npx;
-    uint32_t* vals_out = vals_in + npx;
-    hipLaunchKernelGGL(k_reorder_keys, dim3((npx + 255) / 256), dim3(256), 0, c->stream,
-                       (const float4*)a->pos4, (const float4*)a->nrm4, npx, g.g0[0], g.g0[1], g.g0[2], g.inv_h,
-                       (int)g.n, keys_in, vals_in);
+    // cells: level-lk voxels, at most 2^kMaxCellBits of them (3 bits per level of the code)
+    const uint32_t lgn = (uint32_t)__builtin_ctz(g.n);
+    const uint32_t lk = 3u * lgn > kMaxCellBits ? (3u * lgn - kMaxCellBits + 2u) / 3u : 0u;
+    const uint32_t ncell = 1u << (3u * (lgn - lk));
+    const uint32_t m = ncell + 1u;                          // + the background's counter
+    const uint32_t ntiles = (m + kScanTile - 1u) / kScanTile;
+    void* kv = nullptr;   // [cell | rank | perm] per pixel
+    void* sp = nullptr;   // [counters | tile sums]
+    hipError_t e;
+    if ((e = k4_scratch(c, kScKeys, (size_t)3 * npx * sizeof(uint32_t), &kv, nullptr)) != hipSuccess) return e;
+    if ((e = k4_scratch(c, kScSort, (size_t)(m + ntiles) * sizeof(uint32_t), &sp, nullptr)) != hipSuccess) return e;
+    uint32_t* cell = (uint32_t*)kv;
+    uint32_t* rank = cell + npx;
+    uint32_t* out = rank + npx;
+    uint32_t* cnt = (uint32_t*)sp;
+    uint32_t* tiles = cnt + m;
+    hipStream_t s = c->stream;
+    if ((e = hipMemsetAsync(cnt, 0, (size_t)m * sizeof(uint32_t), s)) != hipSuccess) return e;
+    const uint32_t pblocks = (npx + 255u) / 256u;
+    hipLaunchKernelGGL(k_reorder_count, dim3(pblocks), dim3(256), 0, s, (const float4*)a->pos4,
+                       (const float4*)a->nrm4, npx, g.g0[0], g.g0[1], g.g0[2], g.inv_h, (int)g.n, (int)lk, ncell, cnt,
+                       cell, rank);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(256), 0, s, (const uint32_t*)cnt, m, tiles);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(256), 0, s, tiles, ntiles);
+    hipLaunchKernelGGL(k_scan_down, dim3(ntiles), dim3(256), 0, s, cnt, m, (const uint32_t*)tiles);
+    hipLaunchKernelGGL(k_reorder_scatter, dim3(pblocks), dim3(256), 0, s, (const uint32_t*)cell,
+                       (const uint32_t*)rank, (const uint32_t*)cnt, npx, out);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // bits 0..29: the Morton code (n <= 1024), bit 30: background
-    e = rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out, npx, 0, 31, c->stream);
-    if (e != hipSuccess) return e;
-    *perm = vals_out;
+    *perm = out;
     return hipSuccess;
 }
 

@@ -161,6 +161,7 @@ struct TraceK {
                                  // 2: ndp diffuse parts (cones [g * nd_chunk, ...)) | specular
     int nd_chunk;                // split 2: diffuse cones per part (part g: [g * nd_chunk, (g + 1) * nd_chunk) & nd)
     int ndp;                     // split 2: diffuse parts (>= 2), each followed in blockIdx order by the next
+    int spec_first;              // split 2: the specular part comes first in blockIdx order (variant 0x2000)
     int xcd_g;                   // units per XCD chunk of the workgroup map (0 = one contiguous run per XCD)
     float4* sc_part;             // split 2: [px] diffuse sum after cones [0, nd_chunk)  (per output index)
     float4* sc_cone;             // split 2: [cone - nd_chunk][px] results of cones [nd_chunk, nd)
@@ -208,7 +209,10 @@ __device__ __forceinline__ float4 combine3(float wx, float wy, float wz, float4 
 // corners whose three anisotropic faces are in registers at once (VGPR budget)
 constexpr int kCh = 4;
 // the occupancy form (5 waves/SIMD, 96 VGPRs) keeps 2 corners x 3 faces in flight
-constexpr int kChOcc = 2;
+#ifndef VCT_K4_CHOCC
+#define VCT_K4_CHOCC 2
+#endif
+constexpr int kChOcc = VCT_K4_CHOCC;
 template <bool UNION> constexpr int gather_chunk() { return UNION ? kCh : kChOcc; }
 
 // trilinear corner weights (x fastest), w_c = (wx * wy) * wz
@@ -1109,8 +1113,10 @@ __global__ void __launch_bounds__(64, MINW) k4_trace(TraceK k) {
     // each leaves its data, the last to finish completes the spec's cone-order
     // sum (the same fmaf chain) and writes the output.
     const uint32_t nb = S3 ? gridDim.x / (uint32_t)(k.ndp + 1) : (k.split ? gridDim.x >> 1 : gridDim.x);
-    const uint32_t part = S3 ? blockIdx.x / nb : (blockIdx.x >= nb ? 1u : 0u);
-    const uint32_t b = blockIdx.x - part * nb;
+    const uint32_t rpart = S3 ? blockIdx.x / nb : (blockIdx.x >= nb ? 1u : 0u);   // in blockIdx order
+    const uint32_t b = blockIdx.x - rpart * nb;
+    // its role: S3 parts 0..ndp-1 diffuse, ndp specular (spec_first: the specular part first)
+    const uint32_t part = (S3 && k.spec_first) ? (rpart == 0 ? (uint32_t)k.ndp : rpart - 1u) : rpart;
     // XCD-aware workgroup -> (local tile, 8x8 block) map, bijective for any grid.
     // The hardware hands workgroup b to XCD b & 7.  Units (waves) are dealt to the
     // XCDs in chunks of G consecutive units (the
@@ -1528,6 +1534,7 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     k.split = (k.spec_on && k.nd > 0 && !a->steps_px && !(a->variant & 0x200)) ? 1 : 0;
     k.nd_chunk = (k.nd + 1) / 2;
     k.ndp = 2;
+    k.spec_first = (a->variant & kVarSpecFirst) ? 1 : 0;
     {   // variant bits 16-19: XCD map (0 default; 1 contiguous runs; 2..6: chunks of 1, 4, 16, 64, 256 units)
         static const int g_of[7] = {0, 0, 1, 4, 16, 64, 256};
         const uint32_t m = (a->variant >> 16) & 0xf;

@@ -10,14 +10,16 @@
 //   0x100      no specular step tables
 //   0x200      all cones in one workgroup (no cone split)
 //   0x400      three cone parts (two diffuse + specular), 0x800 two parts
+//   0x2000     split into parts (0x400 / small launches): the specular part first in
+//              blockIdx order (longest waves dispatched first; round 5 re-measures it with
+//              finer diffuse parts, bits 20-23)
 //   0x4000     the counting form without counters
 //   bits 16-19 XCD map: 0 default, 1 contiguous runs, 2..6 chunks of 1/4/16/64/256 units
 //   bits 20-23 diffuse parts of the three-part split (2 default)
 //
 // Retired in round 4 (measured and not kept; the launch returns an
 // error for them): low byte 2 (bricks without the four-face union, superseded by the
-// occupancy form), 3 (row-major lanes), 0x1000 (four waves per workgroup), 0x2000
-// (specular part dispatched first).
+// occupancy form), 3 (row-major lanes), 0x1000 (four waves per workgroup).
 #pragma once
 #include "../../include/vct.h"
 
@@ -25,7 +27,8 @@ namespace vct {
 constexpr uint32_t kVarGathers = 0x01u;
 constexpr uint32_t kVarNoSpecTables = 0x100u, kVarNoSplit = 0x200u, kVarThreeParts = 0x400u, kVarTwoParts = 0x800u;
 constexpr uint32_t kVarCountingForm = 0x4000u;
-constexpr uint32_t kVarRetired = 0x1000u | 0x2000u;
+constexpr uint32_t kVarSpecFirst = 0x2000u;
+constexpr uint32_t kVarRetired = 0x1000u;
 static_assert(VCT_VARIANT_REORDER == 0x8000u && VCT_VARIANT_FORCE_UNION == 0x1000000u &&
                   VCT_VARIANT_FORCE_OCCUPANCY == 0x2000000u && VCT_VARIANT_SCREEN_ORDER == 0x4000000u,
               "public variant bits");
