@@ -1380,3 +1380,53 @@ def test_trace_form_forced_reports_candidate(gpu_ready):
         ctx.trace_device(*gb, w, h, cam.position, d, sp, variant=variant)
         torch.cuda.synchronize()
         assert ctx.trace_form == form, (hex(variant), ctx.trace_form)
+
+
+@pytest.mark.parametrize("world,rank,gbuf", [(1, 0, "scene"), (8, 3, "scene"), (3, 1, "scene"), (1, 0, "rand")])
+def test_longest_first_dispatch_bitexact(gpu_ready, oracle_mod, world, rank, gbuf):
+    """Longest-first dispatch (vct_trace.hip k4_lpt_order): once a workload's candidate is
+    settled, every timed launch records each unit's wave duration and the next one deals
+    each XCD's units longest first.  Every launch -- the recording ones, the reordered ones
+    on one stream and on two alternating streams (whose order tables are per stream while
+    the durations are shared), and with the dispatch off (0x20000000) -- equals the
+    counting launch bit for bit; so does the oracle's frame."""
+    import torch
+    from vct.multi import TILE, tiles_for_rank
+    n, w, h = 64, 320, 192
+    ctx, s, arrs, (g0, E) = gpu_pipeline(n, "atrium")
+    (pos, nrm, alb), cam = _gbuf(gbuf, s, ctx.download_voxels(), g0, E, w, h)
+    dev = torch.device("cuda")
+    main = torch.cuda.current_stream()
+    ctx.set_stream(main.cuda_stream)
+    gb = [torch.from_numpy(a).to(dev) for a in (pos, nrm, alb)]
+    opx = tiles_for_rank(w, h, rank, world) * TILE * TILE if world > 1 else w * h
+    kw = dict(tile_rank=rank, tile_world=world, tile_compact=world > 1)
+
+    def run(variant=0, counted=False, stream=None):
+        d = torch.full((opx, 4), -1.0, device=dev)
+        sp = torch.full((opx, 4), -1.0, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        if stream is not None:
+            stream.wait_stream(main)
+            ctx.set_stream(stream.cuda_stream)
+        ctx.trace_device(*gb, w, h, cam.position, d, sp, cone_steps=cnt if counted else None, variant=variant, **kw)
+        if stream is not None:
+            ctx.set_stream(main.cuda_stream)
+            main.wait_stream(stream)
+        torch.cuda.synchronize()
+        return d.cpu().numpy(), sp.cpu().numpy(), int(cnt[0])
+
+    rd, rs, steps = run(counted=True)
+    if world == 1:
+        ref = oracle_mod.trace(n, g0, E, ctx.download_level(0), gpu_pyramid_flat(ctx), pos, nrm, alb, cam.position)
+        assert np.array_equal(rd.reshape(h, w, 4), ref["diffuse"]) and np.array_equal(rs.reshape(h, w, 4), ref["spec"])
+        assert steps == ref["cone_steps"]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for i in range(48):   # settle the candidate, record, then longest-first launches
+        stream = streams[i % 2] if i >= 32 else None
+        d, sp, _ = run(stream=stream)
+        assert np.array_equal(d, rd) and np.array_equal(sp, rs), (i, stream is not None)
+    assert ctx.trace_form >= 0
+    d, sp, _ = run(variant=0x20000000)
+    assert np.array_equal(d, rd) and np.array_equal(sp, rs)
+    ctx.close()

@@ -333,11 +333,13 @@ void vct_destroy(vct_ctx* c) {
             if (s.p) (void)hipFree(s.p);
     if (c->ev) (void)hipEventDestroy(c->ev);
     if (c->xchg_done) (void)hipEventDestroy(c->xchg_done);
-    for (auto& en : c->k4tune.e)
+    for (auto& en : c->k4tune.e) {
         for (auto& f : en.ev)
             for (auto& sl : f)
                 for (hipEvent_t e : sl)
                     if (e) (void)hipEventDestroy(e);
+        if (en.hist) (void)hipFree(en.hist);
+    }
     if (c->k4tune.prev_end) (void)hipEventDestroy(c->k4tune.prev_end);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

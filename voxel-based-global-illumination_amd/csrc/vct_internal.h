@@ -94,7 +94,7 @@ struct Scratch {
 // K4's per-launch scratch, one set per stream: K4 launches on different streams may run
 // concurrently (a host that overlaps consecutive frames), so the cone-split hand-over
 // and the ray-reorder buffers belong to the stream, not to the context.
-enum { kScFlags = 0, kScHand = 1, kScKeys = 2, kScSort = 3, kScN = 4 };
+enum { kScFlags = 0, kScHand = 1, kScKeys = 2, kScSort = 3, kScOrder = 4, kScN = 5 };
 struct StreamScratch {
     hipStream_t s = nullptr;
     bool used = false;
@@ -159,6 +159,12 @@ struct K4Tuner {
         int seen[4] = {0, 0, 0, 0};           // completed samples (the first one of a first timing is dropped)
         float best[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // fastest completed sample, ms
         hipEvent_t last = nullptr;            // end event of the previous timed launch while timing
+        // longest-first dispatch (launch_trace): the chosen candidate's per-unit wave durations,
+        // recorded by every timed launch; the next one dispatches each XCD's units longest first
+        uint32_t* hist = nullptr;             // [hist_cap] s_memrealtime ticks per unit (device)
+        uint32_t hist_cap = 0, hist_units = 0;
+        int hist_cand = -1;                   // candidate (form | order) the durations belong to
+        bool hist_ok = false;                 // a recording launch has been queued
     };
     Entry e[kEntries];
     int cur = -1;                             // entry of the last launch (vct_trace_form)
@@ -190,6 +196,8 @@ struct vct_ctx {
     vct::StepRow* step_tab = nullptr;   // [kMaxStepRows] diffuse-cone step table (device)
     unsigned* spec_keys = nullptr;      // [2 * kSpecSlots]: specular table keys (~0u free), then states
     vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)
+    const uint32_t* k4_dbg_order = nullptr;   // vct_debug_k4_sched (tools): K4 dispatch order
+    uint32_t* k4_dbg_dur = nullptr;           // and per-unit wave durations
     int* k1_err = nullptr;              // device flag of vct_voxelize_device (index out of range)
     // vct_create_multi: this context is device rank 0 and owns one context per
     // further device (ranks 1..n-1); empty for a single-device context
@@ -241,7 +249,8 @@ hipError_t launch_relayout(vct_ctx* c, const float4* src, float4* dst, uint32_t 
 hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a);
 // ray reordering (variant 0x8000, vct_reorder.hip): *perm = the frame's pixels sorted by the
 // Morton code of their cone origin's voxel, background last (device, w * h entries)
-hipError_t launch_reorder(vct_ctx* c, const vct_trace_args* a, const uint32_t** perm);
+// (perm_spec, nullable: a second order for the specular part, by cell and cone aperture)
+hipError_t launch_reorder(vct_ctx* c, const vct_trace_args* a, const uint32_t** perm, const uint32_t** perm_spec);
 hipError_t launch_untile(vct_ctx* c, const float4* gathered, uint32_t planes, uint32_t w, uint32_t h,
                          uint32_t world, float4* const* frames, bool packed = false);
 // composite + present (row f3)

@@ -16,6 +16,20 @@
 // pixel runs exactly the arithmetic it runs without the reordering, so outputs and step
 // counts are bit-identical whatever the order inside a cell (tested).
 //
+// Two keys (round 5), one permutation each when the launch traces the specular cone in
+// its own part (the parts write different outputs, so each may order the pixels its own
+// way):
+//   diffuse  the level-lk cell, then sign(n.z) -- the branch of the Duff et al. tangent
+//            basis: pixels on either side of it get the ring cones rotated against each
+//            other, so a wave mixing them selects five or six faces and gathers (G_rand
+//            -1.9 % against the cell alone; a coarser cell x the normal's dominant axis
+//            and sign(n.z) was -1.2 %);
+//   specular a cell 8x coarser, then the cone's aperture tau = clamp(roughness) in half
+//            octaves.  A specular cone's mip level is log2(2 tau t): lanes whose tau
+//            differ by more than a fraction of an octave disagree on the level at most
+//            steps, and such a step is gathered per lane at per-lane levels (64-bit
+//            addresses, both levels one after the other).
+//
 // The grouping is a counting sort, hand-written for the job (round 5; it replaced a
 // rocPRIM radix sort of (Morton code, pixel) pairs, four one-sweep passes):
 //   k_reorder_count    per pixel its cell (Morton code at level lk: at most 2^21 cells,
@@ -34,7 +48,10 @@
 namespace vct {
 namespace {
 
-constexpr uint32_t kMaxCellBits = 21;       // at most 2^21 cells (8 MB of counters)
+// key kinds: cell bits and class bits (at most 2^22 counters = 16 MB)
+enum { kKeyDiffuse = 0, kKeySpecular = 1 };
+template <int KIND> constexpr uint32_t key_class_bits() { return KIND == kKeyDiffuse ? 1u : 4u; }
+template <int KIND> constexpr uint32_t key_cell_bits() { return KIND == kKeyDiffuse ? 21u : 18u; }
 constexpr int kScanPer = 16;                // counters per thread in the scan kernels
 constexpr uint32_t kScanTile = 256u * kScanPer;
 
@@ -70,12 +87,23 @@ __device__ __forceinline__ uint32_t block_scan256(uint32_t v, uint32_t& total) {
     return before + incl - v;
 }
 
-// cell of each pixel's cone origin (cells = level-lk voxels in Morton order; background =
-// cell ncell) and its rank among the pixels of that cell
+// aperture class of a specular cone: tau = clamp(roughness, VCT_SPEC_TAU_MIN, VCT_SPEC_TAU_MAX)
+// (as K4 computes it) in half octaves, from its exponent and top mantissa bit
+__device__ __forceinline__ uint32_t tau_class(float rough) {
+    const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
+    const int ex = (int)((__float_as_uint(tau) >> 23) & 0xffu) - 127;   // -6 .. 0
+    const int hc = 2 * (ex + 7) + (int)((__float_as_uint(tau) >> 22) & 1u);
+    return (uint32_t)min(max(hc, 0), 15);
+}
+
+// key of each pixel (cell of its cone origin: level-lk voxels in Morton order, then the
+// kind's class bits; background = key ncell) and its rank among the pixels of that key
+template <int KIND>
 __global__ void __launch_bounds__(256) k_reorder_count(const float4* __restrict__ pos, const float4* __restrict__ nrm,
-                                                       uint32_t npx, float g0x, float g0y, float g0z, float inv_h,
-                                                       int n, int lk, uint32_t ncell, uint32_t* __restrict__ cnt,
-                                                       uint32_t* __restrict__ cell, uint32_t* __restrict__ rank) {
+                                                       const float4* __restrict__ alb, uint32_t npx, float g0x,
+                                                       float g0y, float g0z, float inv_h, int n, int lk, uint32_t ncell,
+                                                       uint32_t* __restrict__ cnt, uint32_t* __restrict__ cell,
+                                                       uint32_t* __restrict__ rank) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     const bool in = i < npx;
     float4 P = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -92,6 +120,8 @@ __global__ void __launch_bounds__(256) k_reorder_count(const float4* __restrict_
             return (uint32_t)(f < 0.0f ? 0 : (f > (float)(n - 1) ? n - 1 : (int)f)) >> lk;
         };
         c = spread3(q(ox)) | (spread3(q(oy)) << 1) | (spread3(q(oz)) << 2);
+        if (KIND == kKeyDiffuse) c = (c << 1) | (N.z < 0.0f ? 1u : 0u);
+        else c = (c << 4) | tau_class(alb[i].w);
         r = atomicAdd(cnt + c, 1u);
     }
     // the background shares one counter: one atomic per wave
@@ -163,38 +193,51 @@ __global__ void __launch_bounds__(256) k_reorder_scatter(const uint32_t* __restr
 
 }  // namespace
 
-hipError_t launch_reorder(vct_ctx* c, const vct_trace_args* a, const uint32_t** perm) {
+// one counting sort of the frame's pixels by key kind KIND into out (npx entries)
+template <int KIND>
+static hipError_t sort_pixels(vct_ctx* c, const vct_trace_args* a, uint32_t* kv, uint32_t* cnt, uint32_t* out) {
     const Grid& g = c->grid;
     const uint32_t npx = a->width * a->height;
-    // cells: level-lk voxels, at most 2^kMaxCellBits of them (3 bits per level of the code)
     const uint32_t lgn = (uint32_t)__builtin_ctz(g.n);
-    const uint32_t lk = 3u * lgn > kMaxCellBits ? (3u * lgn - kMaxCellBits + 2u) / 3u : 0u;
-    const uint32_t ncell = 1u << (3u * (lgn - lk));
+    const uint32_t cb = key_cell_bits<KIND>();
+    const uint32_t lk = 3u * lgn > cb ? (3u * lgn - cb + 2u) / 3u : 0u;   // cells: level-lk voxels
+    const uint32_t ncell = 1u << (3u * (lgn - lk) + key_class_bits<KIND>());
     const uint32_t m = ncell + 1u;                          // + the background's counter
     const uint32_t ntiles = (m + kScanTile - 1u) / kScanTile;
-    void* kv = nullptr;   // [cell | rank | perm] per pixel
-    void* sp = nullptr;   // [counters | tile sums]
-    hipError_t e;
-    if ((e = k4_scratch(c, kScKeys, (size_t)3 * npx * sizeof(uint32_t), &kv, nullptr)) != hipSuccess) return e;
-    if ((e = k4_scratch(c, kScSort, (size_t)(m + ntiles) * sizeof(uint32_t), &sp, nullptr)) != hipSuccess) return e;
-    uint32_t* cell = (uint32_t*)kv;
-    uint32_t* rank = cell + npx;
-    uint32_t* out = rank + npx;
-    uint32_t* cnt = (uint32_t*)sp;
+    uint32_t* cell = kv;
+    uint32_t* rank = kv + npx;
     uint32_t* tiles = cnt + m;
     hipStream_t s = c->stream;
+    hipError_t e;
     if ((e = hipMemsetAsync(cnt, 0, (size_t)m * sizeof(uint32_t), s)) != hipSuccess) return e;
     const uint32_t pblocks = (npx + 255u) / 256u;
-    hipLaunchKernelGGL(k_reorder_count, dim3(pblocks), dim3(256), 0, s, (const float4*)a->pos4,
-                       (const float4*)a->nrm4, npx, g.g0[0], g.g0[1], g.g0[2], g.inv_h, (int)g.n, (int)lk, ncell, cnt,
-                       cell, rank);
+    hipLaunchKernelGGL(k_reorder_count<KIND>, dim3(pblocks), dim3(256), 0, s, (const float4*)a->pos4,
+                       (const float4*)a->nrm4, (const float4*)a->alb4, npx, g.g0[0], g.g0[1], g.g0[2], g.inv_h,
+                       (int)g.n, (int)lk, ncell, cnt, cell, rank);
     hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(256), 0, s, (const uint32_t*)cnt, m, tiles);
     hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(256), 0, s, tiles, ntiles);
     hipLaunchKernelGGL(k_scan_down, dim3(ntiles), dim3(256), 0, s, cnt, m, (const uint32_t*)tiles);
     hipLaunchKernelGGL(k_reorder_scatter, dim3(pblocks), dim3(256), 0, s, (const uint32_t*)cell,
                        (const uint32_t*)rank, (const uint32_t*)cnt, npx, out);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    *perm = out;
+    return hipGetLastError();
+}
+
+hipError_t launch_reorder(vct_ctx* c, const vct_trace_args* a, const uint32_t** perm, const uint32_t** perm_spec) {
+    const uint32_t npx = a->width * a->height;
+    // counters: at most 2^22 + 1, plus the tile sums
+    const size_t mmax = (size_t)(1u << 22) + 1u, tmax = (mmax + kScanTile - 1u) / kScanTile;
+    void* kv = nullptr;   // [cell | rank | perm | perm_spec] per pixel
+    void* sp = nullptr;   // [counters | tile sums]
+    hipError_t e;
+    if ((e = k4_scratch(c, kScKeys, (size_t)4 * npx * sizeof(uint32_t), &kv, nullptr)) != hipSuccess) return e;
+    if ((e = k4_scratch(c, kScSort, (mmax + tmax) * sizeof(uint32_t), &sp, nullptr)) != hipSuccess) return e;
+    uint32_t* base = (uint32_t*)kv;
+    if ((e = sort_pixels<kKeyDiffuse>(c, a, base, (uint32_t*)sp, base + 2 * (size_t)npx)) != hipSuccess) return e;
+    *perm = base + 2 * (size_t)npx;
+    if (perm_spec) {
+        if ((e = sort_pixels<kKeySpecular>(c, a, base, (uint32_t*)sp, base + 3 * (size_t)npx)) != hipSuccess) return e;
+        *perm_spec = base + 3 * (size_t)npx;
+    }
     return hipSuccess;
 }
 

@@ -168,7 +168,10 @@ struct TraceK {
     size_t sc_px;                // pixels per scratch plane
     unsigned* sc_flag;           // split 2: [block][wave] hand-over counter (0 between launches)
     const uint32_t* perm;        // ray reordering (variant 0x8000): lane j of wave u traces pixel perm[64 u + j]
+    const uint32_t* perm_spec;   // the specular part's order (null: perm)
     uint32_t npx;                // its length (w * h)
+    const uint32_t* order;       // dispatch order: workgroup i traces unit order[i] (null: unit i)
+    uint32_t* dur;               // per unit: its wave's duration in s_memrealtime ticks (null: not recorded)
     const uint32_t* zmap;        // Grid::zmap (empty-space maps 1..zm_levels; zm_levels = 0: no test)
     uint32_t zmap_bytes;
     int zm_levels;
@@ -1113,8 +1116,12 @@ __global__ void __launch_bounds__(64, MINW) k4_trace(TraceK k) {
     // each leaves its data, the last to finish completes the spec's cone-order
     // sum (the same fmaf chain) and writes the output.
     const uint32_t nb = S3 ? gridDim.x / (uint32_t)(k.ndp + 1) : (k.split ? gridDim.x >> 1 : gridDim.x);
-    const uint32_t rpart = S3 ? blockIdx.x / nb : (blockIdx.x >= nb ? 1u : 0u);   // in blockIdx order
-    const uint32_t b = blockIdx.x - rpart * nb;
+    // the unit this workgroup traces: blockIdx, or its entry of a dispatch order (a
+    // permutation of the units, e.g. longest first)
+    const uint32_t vb = k.order ? k.order[blockIdx.x] : blockIdx.x;
+    const unsigned long long t_start = k.dur ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const uint32_t rpart = S3 ? vb / nb : (vb >= nb ? 1u : 0u);   // in unit order
+    const uint32_t b = vb - rpart * nb;
     // its role: S3 parts 0..ndp-1 diffuse, ndp specular (spec_first: the specular part first)
     const uint32_t part = (S3 && k.spec_first) ? (rpart == 0 ? (uint32_t)k.ndp : rpart - 1u) : rpart;
     // XCD-aware workgroup -> (local tile, 8x8 block) map, bijective for any grid.
@@ -1167,8 +1174,9 @@ __global__ void __launch_bounds__(64, MINW) k4_trace(TraceK k) {
     uint32_t pix, oidx;                          // w * h < 2^32 (vct_trace_device)
     if (k.perm) {                                // reordered rays: whole frame, outputs at the pixel
         const uint32_t si = (rb * 4u + wave) * 64u + lane;
+        const uint32_t* perm = (k.perm_spec && !do_diff) ? k.perm_spec : k.perm;
         in_frame = si < k.npx;
-        pix = oidx = in_frame ? k.perm[si] : 0u;
+        pix = oidx = in_frame ? perm[si] : 0u;
     } else {
         const uint32_t tile = lt * (uint32_t)k.world + (uint32_t)k.rank;
         const uint32_t x = (tile % (uint32_t)k.tiles_x) * VCT_TILE + px;
@@ -1297,6 +1305,7 @@ __global__ void __launch_bounds__(64, MINW) k4_trace(TraceK k) {
         const uint32_t wt = wave_sum_u32(texels);
         if (lane == 0 && wt) atomicAdd(k.texels_total, (unsigned long long)wt);
     }
+    if (k.dur && lane == 0) k.dur[vb] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
     pc.flush();
 #if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
     {
@@ -1310,6 +1319,51 @@ __global__ void __launch_bounds__(64, MINW) k4_trace(TraceK k) {
         }
     }
 #endif
+}
+
+// Longest-first dispatch (LPT) of a K4 launch.  A unit (workgroup = one 8x8 block of one
+// cone part) runs on XCD unit % 8 (round-robin placement; the XCD map inside k4_trace keeps a
+// tile's units on one XCD), so the order is built per residue class: class x's units
+// {x, x + 8, ...} are bucketed by their last recorded duration (log2 with four steps per
+// octave, longest bucket first) and dealt to the class's workgroups x + 8 i in that order.
+// Each unit's duration is read once (a concurrent frame may be rewriting it: any values
+// give a permutation), so the result is always a permutation of the units and the frame's
+// outputs are those of blockIdx order (every unit runs the same arithmetic wherever it is
+// dispatched).  Measured (tools/lpt_emul.py, same-frame durations): one rank of 8 at 1080p
+// 0.234 -> 0.201 ms, one of 4 0.392 -> 0.364 ms, the full C3 frame 1.109 -> 1.073 ms.
+constexpr uint32_t kLptBuckets = 128;
+constexpr uint32_t kLptMaxPerClass = 48u * 1024u;   // key bytes per class in LDS
+__global__ void __launch_bounds__(1024) k4_lpt_order(const uint32_t* __restrict__ dur, uint32_t units,
+                                                     uint32_t* __restrict__ order) {
+    extern __shared__ uint8_t key[];              // per unit of this class
+    __shared__ uint32_t off[kLptBuckets];
+    const uint32_t x = blockIdx.x, tid = threadIdx.x;
+    const uint32_t nc = units > x ? (units - x + 7u) / 8u : 0u;
+    for (uint32_t i = tid; i < kLptBuckets; i += 1024u) off[i] = 0u;
+    __syncthreads();
+    for (uint32_t j = tid; j < nc; j += 1024u) {
+        const uint32_t d = dur[x + 8u * j] | 1u;
+        const uint32_t lg = 31u - (uint32_t)__builtin_clz(d);
+        const uint32_t sub = lg >= 2u ? (d >> (lg - 2u)) & 3u : 0u;
+        const uint32_t bk = min(4u * lg + sub, kLptBuckets - 1u);
+        const uint8_t kk = (uint8_t)(kLptBuckets - 1u - bk);   // the longest first
+        key[j] = kk;
+        atomicAdd(&off[kk], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (uint32_t i = 0; i < kLptBuckets; ++i) {
+            const uint32_t t = off[i];
+            off[i] = run;
+            run += t;
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < nc; j += 1024u) {
+        const uint32_t pos = atomicAdd(&off[key[j]], 1u);
+        order[x + 8u * pos] = x + 8u * j;
+    }
 }
 
 }  // namespace
@@ -1384,6 +1438,8 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
         e.retimes = 0;
         e.epoch = c->grid_epoch;
         e.epoch_wait = K4Tuner::kEpochMin;
+        e.hist_ok = false;                       // another workload's durations
+        e.hist_cand = -1;
     }
     K4Tuner::Entry& t = T.e[ix];
     t.used = ++T.clock;
@@ -1541,7 +1597,9 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         k.xcd_g = g_of[m < 7 ? m : 0];
     }
     k.sc_part = k.sc_cone = nullptr; k.sc_flag = nullptr; k.sc_px = 0;
-    k.perm = nullptr;
+    k.perm = k.perm_spec = nullptr;
+    k.order = c->k4_dbg_order;
+    k.dur = c->k4_dbg_dur;
     k.npx = a->width * a->height;
     k.zmap = g.zm_valid ? g.zmap : nullptr;
     k.zm_levels = g.zm_valid ? g.zm_levels : 0;
@@ -1592,7 +1650,8 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     if (cand & 2) {
         // ray reordering (full frame, one rank): waves take 64 consecutive entries of the
         // sorted pixel list; nlt counts 64-wave units of it instead of 64x64 tiles
-        hipError_t e = launch_reorder(c, a, &k.perm);
+        // the specular part (split launches) gets its own order by cell and cone aperture
+        hipError_t e = launch_reorder(c, a, &k.perm, (k.split && k.spec_on && !(a->variant & kVarOnePerm)) ? &k.perm_spec : nullptr);
         if (e != hipSuccess) return e;
         nlt = (k.npx + 64u * 64u - 1u) / (64u * 64u);
     }
@@ -1630,6 +1689,40 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         // 4K 6.91 -> 6.15 ms, one rank of 8: 0.288 -> 0.265 ms)
         k.xcd_g = blocks / nparts >= 16384u ? 64 : 16;
     }
+    // longest-first dispatch for the timed launches of a settled default workload (not
+    // while its candidates are being timed), from the durations its previous launch recorded
+    if (deflt && !cnt_form && !(a->variant & kVarNoLpt) && c->k4tune.cur >= 0 && !c->k4_dbg_order && !c->k4_dbg_dur &&
+        blocks / 8u <= kLptMaxPerClass) {
+        K4Tuner::Entry& te = c->k4tune.e[c->k4tune.cur];
+        if (te.chosen >= 0) {
+            if (te.hist_cap < blocks) {
+                if (te.hist) {
+                    hipError_t e = hipStreamSynchronize(c->stream);   // a launch may still write it
+                    if (e != hipSuccess) return e;
+                    (void)hipFree(te.hist);
+                    te.hist = nullptr;
+                    te.hist_cap = 0;
+                }
+                hipError_t e = hipMalloc((void**)&te.hist, (size_t)blocks * sizeof(uint32_t));
+                if (e != hipSuccess) return e;
+                te.hist_cap = blocks;
+                te.hist_ok = false;
+            }
+            if (te.hist_units != blocks || te.hist_cand != cand) te.hist_ok = false;
+            if (te.hist_ok) {
+                void* op = nullptr;
+                hipError_t e = k4_scratch(c, kScOrder, (size_t)blocks * sizeof(uint32_t), &op, nullptr);
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL(k4_lpt_order, dim3(8), dim3(1024), (blocks + 7u) / 8u, c->stream,
+                                   (const uint32_t*)te.hist, blocks, (uint32_t*)op);
+                k.order = (const uint32_t*)op;
+            }
+            k.dur = te.hist;
+            te.hist_units = blocks;
+            te.hist_cand = cand;
+            te.hist_ok = true;
+        }
+    }
     // O32 instantiations need every level below 4 GiB: n <= 512
     const bool o32 = g.n <= 512;
 #define VCT_K4(BRICK, MINW, UNION, CNT)                                                                 \
@@ -1664,6 +1757,15 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
 }
 
 }  // namespace vct
+
+// Test / tool hook (not part of include/vct.h): the following launches trace unit order[i]
+// in workgroup i and record each unit's duration into dur (device pointers, null = off).
+extern "C" int vct_debug_k4_sched(vct_ctx* c, const uint32_t* order, uint32_t* dur) {
+    if (!c) return -1;
+    c->k4_dbg_order = order;
+    c->k4_dbg_dur = dur;
+    return 0;
+}
 
 #if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
 extern "C" int vct_debug_waves(unsigned long long* out, int n) {   // out[n][3]; n <= 1 << 18
