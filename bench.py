@@ -1075,7 +1075,9 @@ def run(args, world):
         result["overlap_tune"] = m["overlap_tune"]
         result["k4_form"] = form_name(m["k4_form"])
         result["k4_dispatch"] = {
-            "order": "each XCD's units longest first, from the previous launch's per-unit wave durations",
+            "order": "blockIdx order through the XCD map; each XCD's units longest first (from the previous "
+                     "launch's per-unit wave durations) only in launches of <= 4 generations of waves that do "
+                     "not overlap another frame (a multi-GPU rank's share)",
             "k4_kernel_ms_avg_blockidx_order": round(m["k4_kernel_ms_avg_blockidx_order"], 4)
             if m["k4_kernel_ms_avg_blockidx_order"] else None}
         for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "k3_mips_relight_ms", "grid_bcast_ms", "frame_relight_ms",

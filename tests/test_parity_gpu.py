@@ -83,12 +83,14 @@ def test_voxelize_packed_sums_fallback(gpu_ready, oracle_mod, case):
 @pytest.mark.parametrize("name,n", [("atrium", 128), ("atrium", 256), ("courtyard", 256)])
 def test_inject_bitexact_coarse_bricks(gpu_ready, oracle_mod, name, n):
     """K2 where the shadow walk's coarse bricks hold 2^3 / 4^3 voxels (n = 128 / 256; the
-    sizes above use one voxel per brick): level 0 equals the oracle's inject of the GPU's
-    own voxels bit for bit, for the scene light and for a light with a zero component."""
+    sizes above use one voxel per brick) and the walk skips empty ones whole (round 5):
+    level 0 equals the oracle's inject of the GPU's own voxels bit for bit, for the scene
+    light, lights with one and two zero components (axis-parallel walks) and the diagonal
+    (equal t on all three axes at every step: the tie order decides every cell)."""
     from vct import scenes
     ctx, s, _, _ = gpu_pipeline(n, name)
     ao, nm = ctx.download_voxels()
-    for light in (scenes.LIGHT_DIR, (0.0, 1.0, -0.35)):
+    for light in (scenes.LIGHT_DIR, (0.0, 1.0, -0.35), (0.0, 1.0, 0.0), (1.0, 1.0, 1.0), (-0.4, 0.7, 0.3)):
         ctx.inject_directional(light, scenes.LIGHT_COLOR)
         ref = oracle_mod.inject(n, ao, nm, light, scenes.LIGHT_COLOR)
         assert np.array_equal(ctx.download_level(0), ref), f"K2 radiance differs (light {light})"
@@ -1387,8 +1389,8 @@ def test_longest_first_dispatch_bitexact(gpu_ready, oracle_mod, world, rank, gbu
     """Longest-first dispatch (vct_trace.hip k4_lpt_order): once a workload's candidate is
     settled, every timed launch records each unit's wave duration and the next one deals
     each XCD's units longest first.  Every launch -- the recording ones, the reordered ones
-    on one stream and on two alternating streams (whose order tables are per stream while
-    the durations are shared), and with the dispatch off (0x20000000) -- equals the
+    on one stream and, forced by 0x10000000, on two alternating streams (whose order tables
+    are per stream while the durations are shared), and with the dispatch off (0x20000000) -- equals the
     counting launch bit for bit; so does the oracle's frame."""
     import torch
     from vct.multi import TILE, tiles_for_rank
@@ -1424,7 +1426,8 @@ def test_longest_first_dispatch_bitexact(gpu_ready, oracle_mod, world, rank, gbu
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     for i in range(48):   # settle the candidate, record, then longest-first launches
         stream = streams[i % 2] if i >= 32 else None
-        d, sp, _ = run(stream=stream)
+        # overlapped launches dispatch longest first only when 0x10000000 asks for it
+        d, sp, _ = run(variant=0x10000000 if i >= 32 else 0, stream=stream)
         assert np.array_equal(d, rd) and np.array_equal(sp, rs), (i, stream is not None)
     assert ctx.trace_form >= 0
     d, sp, _ = run(variant=0x20000000)

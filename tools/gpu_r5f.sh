@@ -9,9 +9,15 @@ timeout -k 10 500 python -u -m pytest -x -q --timeout 300 --timeout-method threa
   tests/test_parity_gpu.py::test_frame_pipeline_equals_full_frames tests/test_parity_gpu.py::test_reorder_equals_screen_order \
   tests/test_parity_gpu.py::test_reordered_frames_overlapped tests/test_parity_gpu.py::test_trace_form_tuner \
   tests/test_parity_gpu.py::test_tiled_trace_equals_full_frame tests/test_parity_gpu.py::test_multi_device_context \
+  tests/test_parity_gpu.py::test_inject_bitexact_coarse_bricks tests/test_parity_gpu.py::test_voxelize_inject_mips_bitexact \
+  tests/test_parity_gpu.py::test_mips_relight_sparse_bitexact tests/test_dump.py \
   tests/test_parity_full.py > gpurun_out/t_r5f.log 2>&1
 rc=$?; echo "parity: $(tail -1 gpurun_out/t_r5f.log)"; [ $rc -eq 0 ] || { grep -E "FAIL|Error" gpurun_out/t_r5f.log | head; exit $rc; }
 for sc in atrium courtyard; do
+  for sk in 1 0 1 0; do
+    VCT_K2_SKIP=$sk timeout -k 10 120 python tools/k2_bench.py --scene $sc > gpurun_out/k2_${sc}_${sk}.log 2>&1 || { tail -3 gpurun_out/k2_${sc}_${sk}.log; exit 1; }
+    echo "k2 $sc skip=$sk: $(tail -1 gpurun_out/k2_${sc}_${sk}.log)"
+  done
   timeout -k 10 300 python tools/ab.py --variants 0,0x20000000 --rounds 7 --scene $sc 2>/dev/null > gpurun_out/ab_lpt_$sc.json || exit 1
   echo "$sc: $(python -c "import json;d=json.load(open('gpurun_out/ab_lpt_$sc.json'));print({k:(v['median_ms'],v['bitexact_vs_first']) for k,v in d['variants'].items()}, d['k4_form'])")"
 done

@@ -183,6 +183,7 @@ struct K4Tuner {
 struct vct_ctx {
     vct_config cfg{};
     int device = 0;
+    int n_cu = 0;                       // the device's compute units (queried on first use)
     hipStream_t stream = nullptr;
     vct::Grid grid;
     vct::Mesh mesh;

@@ -1331,6 +1331,7 @@ __global__ void __launch_bounds__(64, MINW) k4_trace(TraceK k) {
 // outputs are those of blockIdx order (every unit runs the same arithmetic wherever it is
 // dispatched).  Measured (tools/lpt_emul.py, same-frame durations): one rank of 8 at 1080p
 // 0.234 -> 0.201 ms, one of 4 0.392 -> 0.364 ms, the full C3 frame 1.109 -> 1.073 ms.
+constexpr uint32_t kLptMaxGenerations = 4;       // LPT for launches of <= 4 x (CUs x 20) waves
 constexpr uint32_t kLptBuckets = 128;
 constexpr uint32_t kLptMaxPerClass = 48u * 1024u;   // key bytes per class in LDS
 __global__ void __launch_bounds__(1024) k4_lpt_order(const uint32_t* __restrict__ dur, uint32_t units,
@@ -1363,6 +1364,87 @@ __global__ void __launch_bounds__(1024) k4_lpt_order(const uint32_t* __restrict_
     for (uint32_t j = tid; j < nc; j += 1024u) {
         const uint32_t pos = atomicAdd(&off[key[j]], 1u);
         order[x + 8u * pos] = x + 8u * j;
+    }
+}
+
+// Longest-first with locality: a STABLE partition of each class into kLptParts duration
+// bands below the class's longest unit (>= max / 2, >= max / 4, >= max / 8, the rest),
+// longest band first, each band in blockIdx order.  The plain bucket sort above scatters a
+// tile's units over the whole launch (its L2 locality: the courtyard +2 %, the pipelined
+// C3 frame +3 %); inside a band the units keep the XCD map's tile order.
+constexpr int kLptParts = 4;
+constexpr int kLptRounds = 32;                   // units per class <= 32 x 1024 (a 4K frame: 32 640)
+__device__ __forceinline__ uint32_t lpt_band(uint32_t d, uint32_t dmax) {
+    // floor(log2(dmax / d)) clamped to the bands, from the leading-bit positions (+1 when
+    // d's mantissa exceeds dmax's shifted down: exact for the band edges dmax / 2^k)
+    const uint32_t dd = d | 1u;
+    int k = (int)__builtin_clz(dd) - (int)__builtin_clz(dmax | 1u);
+    if (k >= 0 && ((dmax | 1u) >> k) > dd) ++k;   // d below dmax >> k: one band further
+    return (uint32_t)min(max(k, 0), kLptParts - 1);
+}
+
+__global__ void __launch_bounds__(1024) k4_lpt_bands(const uint32_t* __restrict__ dur, uint32_t units,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t wmax[16], wc[16][kLptParts], base[kLptParts], run[kLptParts], rt[kLptParts];
+    const uint32_t x = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t nc = units > x ? (units - x + 7u) / 8u : 0u;
+    uint32_t m = 0;
+    for (uint32_t j = tid; j < nc; j += 1024u) m = max(m, dur[x + 8u * j]);
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    if (lane == 0) wmax[wave] = m;
+    if (tid < kLptParts) base[tid] = run[tid] = 0u;
+    __syncthreads();
+    uint32_t dmax = 0;
+    for (int w = 0; w < 16; ++w) dmax = max(dmax, wmax[w]);
+    // each unit's band from ONE read of its duration (a concurrent frame may be rewriting
+    // it: the bands counted and the bands placed must be the same), kept in registers; the
+    // band sizes first, then the units placed round by round (1024 consecutive units a round)
+    __shared__ uint8_t keys[kLptRounds * 1024];
+    const uint32_t rounds = (nc + 1023u) / 1024u;   // <= kLptRounds (launch_trace)
+    for (uint32_t j = tid; j < nc; j += 1024u) {
+        const uint32_t k = lpt_band(dur[x + 8u * j], dmax);
+        keys[j] = (uint8_t)k;
+        atomicAdd(&run[k], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < kLptParts; ++k) {
+            base[k] = acc;
+            acc += run[k];
+            run[k] = 0u;
+        }
+    }
+    __syncthreads();
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t j = r * 1024u + tid;
+        const uint32_t key = j < nc ? (uint32_t)keys[j] : (uint32_t)kLptParts;
+        unsigned long long mine = 0ull;
+#pragma unroll
+        for (int k = 0; k < kLptParts; ++k) {
+            const unsigned long long b = __builtin_amdgcn_ballot_w64(key == (uint32_t)k);
+            if (lane == 0) wc[wave][k] = (uint32_t)__builtin_popcountll(b);
+            if (key == (uint32_t)k) mine = b;
+        }
+        __syncthreads();
+        if (tid < kLptParts) {
+            uint32_t acc = 0;
+            for (int w = 0; w < 16; ++w) {
+                const uint32_t t = wc[w][tid];
+                wc[w][tid] = acc;
+                acc += t;
+            }
+            rt[tid] = acc;
+        }
+        __syncthreads();
+        if (j < nc) {
+            const uint32_t pos = base[key] + run[key] + wc[wave][key] +
+                                 __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+            order[x + 8u * pos] = x + 8u * j;
+        }
+        __syncthreads();
+        if (tid < kLptParts) run[tid] += rt[tid];
+        __syncthreads();
     }
 }
 
@@ -1690,9 +1772,16 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         k.xcd_g = blocks / nparts >= 16384u ? 64 : 16;
     }
     // longest-first dispatch for the timed launches of a settled default workload (not
-    // while its candidates are being timed), from the durations its previous launch recorded
+    // while its candidates are being timed), from the durations its previous launch recorded;
+    // only for launches of at most kLptMaxGenerations generations of waves (a multi-GPU
+    // rank's share) that do not overlap another frame: a large launch balances its own tail
+    // and a concurrent frame fills it (measured: C3 frame +2 %, pipelined +2 %, one rank of 4
+    // -6 %, of 8 -3 %)
+    if (!c->n_cu && hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
+        c->n_cu = 0;
+    const bool lpt_size = c->n_cu > 0 && blocks <= (uint32_t)c->n_cu * 4u * kOccWaves * kLptMaxGenerations;
     if (deflt && !cnt_form && !(a->variant & kVarNoLpt) && c->k4tune.cur >= 0 && !c->k4_dbg_order && !c->k4_dbg_dur &&
-        blocks / 8u <= kLptMaxPerClass) {
+        blocks / 8u <= kLptMaxPerClass && !c->k4tune.multi && (lpt_size || (a->variant & kVarLptAll))) {
         K4Tuner::Entry& te = c->k4tune.e[c->k4tune.cur];
         if (te.chosen >= 0) {
             if (te.hist_cap < blocks) {
@@ -1713,8 +1802,12 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
                 void* op = nullptr;
                 hipError_t e = k4_scratch(c, kScOrder, (size_t)blocks * sizeof(uint32_t), &op, nullptr);
                 if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(k4_lpt_order, dim3(8), dim3(1024), (blocks + 7u) / 8u, c->stream,
-                                   (const uint32_t*)te.hist, blocks, (uint32_t*)op);
+                if ((a->variant & kVarLptSort) || blocks / 8u > (uint32_t)kLptRounds * 1024u)
+                    hipLaunchKernelGGL(k4_lpt_order, dim3(8), dim3(1024), (blocks + 7u) / 8u, c->stream,
+                                       (const uint32_t*)te.hist, blocks, (uint32_t*)op);
+                else
+                    hipLaunchKernelGGL(k4_lpt_bands, dim3(8), dim3(1024), 0, c->stream, (const uint32_t*)te.hist,
+                                       blocks, (uint32_t*)op);
                 k.order = (const uint32_t*)op;
             }
             k.dur = te.hist;

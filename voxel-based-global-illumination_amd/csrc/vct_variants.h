@@ -16,8 +16,11 @@
 //   0x4000     the counting form without counters
 //   bits 16-19 XCD map: 0 default, 1 contiguous runs, 2..6 chunks of 1/4/16/64/256 units
 //   bits 20-23 diffuse parts of the three-part split (2 default)
+//   0x10000000 longest-first dispatch for every settled launch (default: launches of at
+//              most four generations of waves that do not overlap another frame)
 //   0x20000000 no longest-first dispatch (units in blockIdx order)
 //   0x40000000 ray reordering: one order for every cone part (no specular order)
+//   0x80000000 longest-first dispatch as a full bucket sort (default: four stable bands)
 //
 // Retired in round 4 (measured and not kept; the launch returns an
 // error for them): low byte 2 (bricks without the four-face union, superseded by the
@@ -30,8 +33,10 @@ constexpr uint32_t kVarGathers = 0x01u;
 constexpr uint32_t kVarNoSpecTables = 0x100u, kVarNoSplit = 0x200u, kVarThreeParts = 0x400u, kVarTwoParts = 0x800u;
 constexpr uint32_t kVarCountingForm = 0x4000u;
 constexpr uint32_t kVarSpecFirst = 0x2000u;
+constexpr uint32_t kVarLptAll = 0x10000000u;
 constexpr uint32_t kVarNoLpt = 0x20000000u;
 constexpr uint32_t kVarOnePerm = 0x40000000u;
+constexpr uint32_t kVarLptSort = 0x80000000u;
 constexpr uint32_t kVarRetired = 0x1000u;
 static_assert(VCT_VARIANT_REORDER == 0x8000u && VCT_VARIANT_FORCE_UNION == 0x1000000u &&
                   VCT_VARIANT_FORCE_OCCUPANCY == 0x2000000u && VCT_VARIANT_SCREEN_ORDER == 0x4000000u,
