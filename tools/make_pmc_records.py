@@ -32,7 +32,8 @@ sys.path.insert(0, REPO)
 TIMED = re.compile(r"k4_trace<[^>]*, false(?:, \d+)?>\(")   # the counter-free form (any waves per workgroup)
 # kernels of each relight call (vct_voxelize.hip, vct_mips.hip); k2_list builds K1's occupied list
 STAGES = {
-    "k1": re.compile(r"^(?:void )?(?:vct::\(anonymous namespace\)::)?(k1_\w+|k_scan_\w+|k2_list)\b"),
+    # K1's scans are the 64-bit ones (vct_reorder.hip's counting sort has k_scan_* of 32 bits)
+    "k1": re.compile(r"^(?:void )?(?:vct::\(anonymous namespace\)::)?(k1_\w+|k_scan_\w+(?=\(unsigned long long)|k2_list)\b"),
     "k2": re.compile(r"^(?:void )?(?:vct::\(anonymous namespace\)::)?(k2_(?:coarse|shade|walk|inject)\w*)"),
     "k3": re.compile(r"^(?:void )?(?:vct::\(anonymous namespace\)::)?(k3_\w+)"),
 }
