@@ -226,8 +226,9 @@ vct_status vct_trace_device(vct_ctx* ctx, const vct_trace_args* args);
  * the new scene keeps the winner).  While launches alternate streams (overlapped frames;
  * until 64 launches after the last switch) they are not watched, and a timing launch
  * then also waits for the previous launch of any stream.
- * Once the choice is settled, every counter-free launch of the workload records each work
- * unit's (8x8 block x cone part) wave duration, and the next one dispatches each XCD's units
+ * Once the choice is settled, a counter-free launch of at most four generations of waves
+ * that does not overlap another frame (a multi-GPU rank's share) records each work unit's
+ * (8x8 block x cone part) wave duration, and the next such one dispatches each XCD's units
  * longest first from them (a permutation of the units: outputs unchanged).
  * Returns the kept candidate of the last traced workload -- bit 0 the form (0 union,
  * 1 occupancy), bit 1 ray reordering; a forced candidate when the variant fixes both --
