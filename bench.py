@@ -711,22 +711,10 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     k4_ms = [a.elapsed_time(b) for a, b in iev]
     k4_avg_ms = sum(k4_ms) / len(k4_ms)
     k4_med_ms = sorted(k4_ms)[len(k4_ms) // 2]
-    # the same launches with the units in blockIdx order (variant 0x20000000: no longest-first
-    # dispatch from the previous launch's wave durations), for the dispatch's share
-    k4_bo_ms = None
-    if args.variant == 0:
-        for s in range(args.steps):
-            iev[s][0].record(stream)
-            tracer.trace_local(gb, eye, variant=0x20000000)
-            iev[s][1].record(stream)
-        torch.cuda.synchronize()
-        k4_bo_ms = sum(a.elapsed_time(b) for a, b in iev) / args.steps
-        k4_bo_ms = max_over_ranks(torch, dist, dev, [k4_bo_ms], world)[0]
     ms_per_step = elapsed / args.steps * 1e3
     r.update({
         "value": frame_steps * args.steps / elapsed / 1e6, "ms_per_step": ms_per_step, "frame_cone_steps": frame_steps,
         "valid_px": frame_valid, "k4_kernel_ms_avg": k4_avg_ms, "k4_kernel_ms_median": k4_med_ms,
-        "k4_kernel_ms_avg_blockidx_order": k4_bo_ms,
         "k4_kernel_ms_avg_overlapped": sum(k4_ov_ms) / len(k4_ov_ms), "overlap": tracer.overlap,
         "local_texels": local_texels, "local_valid": local_valid, "local_steps": local_steps,
         "frame_relight_ms": round(min(k2_ms + bcast_ms + k3_ms, k2_rep_ms + k3_rep_ms) + ms_per_step, 3),
@@ -1074,12 +1062,10 @@ def run(args, world):
         result["frame_overlap"] = "two trace streams" if m["overlap"] else "one stream"
         result["overlap_tune"] = m["overlap_tune"]
         result["k4_form"] = form_name(m["k4_form"])
-        result["k4_dispatch"] = {
-            "order": "blockIdx order through the XCD map; each XCD's units longest first (from the previous "
-                     "launch's per-unit wave durations) only in launches of <= 4 generations of waves that do "
-                     "not overlap another frame (a multi-GPU rank's share)",
-            "k4_kernel_ms_avg_blockidx_order": round(m["k4_kernel_ms_avg_blockidx_order"], 4)
-            if m["k4_kernel_ms_avg_blockidx_order"] else None}
+        # (the timed loops here overlap frames or follow overlapped ones: blockIdx order)
+        result["k4_dispatch"] = ("blockIdx order through the XCD map; each XCD's units longest first (from the "
+                                 "previous launch's per-unit wave durations) only in launches of <= 4 generations of "
+                                 "waves that do not overlap another frame (DESIGN 13.5)")
         for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "k3_mips_relight_ms", "grid_bcast_ms", "frame_relight_ms",
                    "frame_relight_bcast_ms", "frame_relight_replicated_ms", "replicated_k2_equals_bcast",
                    "trace_ms_max_rank", "gather_ms", "allgather_ms", "k1_roofline", "k2_roofline", "k3_roofline"):

@@ -1786,7 +1786,9 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
         if (te.chosen >= 0) {
             if (te.hist_cap < blocks) {
                 if (te.hist) {
-                    hipError_t e = hipStreamSynchronize(c->stream);   // a launch may still write it
+                    // a launch on any stream may still write it (the durations are shared by the
+                    // streams; only an entry taken over by a larger workload gets here)
+                    hipError_t e = hipDeviceSynchronize();
                     if (e != hipSuccess) return e;
                     (void)hipFree(te.hist);
                     te.hist = nullptr;
