@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--variant", type=lambda x: int(x, 0), default=0)
     ap.add_argument("--scene", default="atrium")
+    ap.add_argument("--streams", type=int, default=2, help="trace streams of the overlapped frames (<= 3)")
+    ap.add_argument("--overlap1", action="store_true", help="overlapped frames at world size 1 too (whole frames)")
     ap.add_argument("--pmc-world", type=int, default=0)
     ap.add_argument("--pmc-rank", type=int, default=0)
     ap.add_argument("--pmc-launches", type=int, default=20)
@@ -96,13 +98,14 @@ def main():
     # (streams made per world size land on hardware queues in turn; GPU_MAX_HW_QUEUES = 4,
     # and two trace streams sharing one queue serialise: measured 4-rank overlapped 0.29 ms
     # after one world size, 0.37-0.39 ms after two)
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    streams = [torch.cuda.Stream() for _ in range(a.streams)]
+    S = a.streams
     for W in [int(x) for x in a.worlds.split(",")]:
         maxt = tiles_for_rank(a.w, a.h, 0, W)
         buf = torch.empty((2, maxt * TILE * TILE, 4), device=dev)
         per = []
         ov = []
-        bufs = [torch.empty((2, maxt * TILE * TILE, 4), device=dev) for _ in range(2)]
+        bufs = [torch.empty((2, maxt * TILE * TILE, 4), device=dev) for _ in range(S)]
         frames = 40
         # each rank's single launch, then its overlapped frames, back to back: a rank process
         # has this one workload (the context keeps four; eight ranks' keys in turn would
@@ -113,19 +116,20 @@ def main():
             per.append(timed(lambda: ctx.trace_device(*gb, a.w, a.h, cam.position, buf[0], buf[1], tile_rank=r,
                                                       tile_world=W, tile_compact=W > 1, variant=a.variant),
                              min_calls=72))
-            if W > 1:
+            if W > 1 or a.overlap1:
                 def loop():
+                    # S frames in flight: frame f on stream f % S starts once frame f - S + 1 ended
                     for f in range(frames):
-                        st = streams[f % 2]
+                        st = streams[f % S]
                         st.wait_stream(stream)
                         ctx.set_stream(st.cuda_stream)
-                        b = bufs[f % 2]
+                        b = bufs[f % S]
                         ctx.trace_device(*gb, a.w, a.h, cam.position, b[0], b[1], tile_rank=r, tile_world=W,
                                          tile_compact=True, variant=a.variant)
                         ctx.set_stream(stream.cuda_stream)
-                        stream.wait_stream(streams[(f + 1) % 2])
-                    stream.wait_stream(streams[0])
-                    stream.wait_stream(streams[1])
+                        stream.wait_stream(streams[(f + 1) % S])
+                    for st_ in streams:
+                        stream.wait_stream(st_)
                 ov.append(timed(loop) / frames)
         gath = torch.empty((W, 2, maxt * TILE * TILE, 4), device=dev)
         fr = (torch.empty((a.h, a.w, 4), device=dev), torch.empty((a.h, a.w, 4), device=dev))
