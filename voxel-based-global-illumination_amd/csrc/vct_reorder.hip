@@ -24,8 +24,9 @@
 //            other, so a wave mixing them selects five or six faces and gathers (G_rand
 //            -1.9 % against the cell alone; a coarser cell x the normal's dominant axis
 //            and sign(n.z) was -1.2 %);
-//   specular a cell 8x coarser, then the cone's aperture tau = clamp(roughness) in half
-//            octaves.  A specular cone's mip level is log2(2 tau t): lanes whose tau
+//   specular a cell 64x coarser (8^3 voxels at 256^3), then the cone's aperture tau =
+//            clamp(roughness) in half octaves: more pixels per (cell, aperture) key, so more
+//            waves whose lanes share one tau (one step table, wave-uniform levels).  A specular cone's mip level is log2(2 tau t): lanes whose tau
 //            differ by more than a fraction of an octave disagree on the level at most
 //            steps, and such a step is gathered per lane at per-lane levels (64-bit
 //            addresses, both levels one after the other).
@@ -51,7 +52,13 @@ namespace {
 // key kinds: cell bits and class bits (at most 2^22 counters = 16 MB)
 enum { kKeyDiffuse = 0, kKeySpecular = 1 };
 template <int KIND> constexpr uint32_t key_class_bits() { return KIND == kKeyDiffuse ? 1u : 4u; }
-template <int KIND> constexpr uint32_t key_cell_bits() { return KIND == kKeyDiffuse ? 21u : 18u; }
+#ifndef VCT_KEY_DIFF_BITS
+#define VCT_KEY_DIFF_BITS 21
+#endif
+#ifndef VCT_KEY_SPEC_BITS
+#define VCT_KEY_SPEC_BITS 15   // level-3 cells at 256^3 (measured on G_rand, ms per frame: 18 bits 6.46,
+#endif                         // 15 bits 5.96, 12 bits 6.08, 9 bits 6.91)
+template <int KIND> constexpr uint32_t key_cell_bits() { return KIND == kKeyDiffuse ? VCT_KEY_DIFF_BITS : VCT_KEY_SPEC_BITS; }
 constexpr int kScanPer = 16;                // counters per thread in the scan kernels
 constexpr uint32_t kScanTile = 256u * kScanPer;
 
