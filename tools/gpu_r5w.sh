@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 5: specular reorder key, aperture-major (tm15 / tm18 cell bits) vs cell-major (shipped, 15 bits), G_rand
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+V=voxel-based-global-illumination_amd/vct
+for lib in libvct_hip.so libvct_hip_tm15.so libvct_hip_tm18.so libvct_hip.so libvct_hip_tm15.so libvct_hip_tm18.so; do
+  VCT_LIB=$V/$lib timeout -k 10 200 python tools/ab.py --variants 0,0x1008000 --rounds 3 --gbuffer rand 2>/dev/null > gpurun_out/ab_w_$lib.json || exit 1
+  echo "rand $lib: $(python -c "import json;d=json.load(open('gpurun_out/ab_w_$lib.json'));print({k:(v['median_ms'],v['bitexact_vs_first']) for k,v in d['variants'].items()}, d['k4_form'])")"
+done

@@ -19,14 +19,16 @@
 // Two keys (round 5), one permutation each when the launch traces the specular cone in
 // its own part (the parts write different outputs, so each may order the pixels its own
 // way):
-//   diffuse  the level-lk cell, then sign(n.z) -- the branch of the Duff et al. tangent
-//            basis: pixels on either side of it get the ring cones rotated against each
-//            other, so a wave mixing them selects five or six faces and gathers (G_rand
-//            -1.9 % against the cell alone; a coarser cell x the normal's dominant axis
-//            and sign(n.z) was -1.2 %);
-//   specular a cell 64x coarser (8^3 voxels at 256^3), then the cone's aperture tau =
-//            clamp(roughness) in half octaves: more pixels per (cell, aperture) key, so more
-//            waves whose lanes share one tau (one step table, wave-uniform levels).  A specular cone's mip level is log2(2 tau t): lanes whose tau
+//   diffuse  sign(n.z) -- the branch of the Duff et al. tangent basis: pixels on either
+//            side of it get the ring cones rotated against each other, so a wave mixing them
+//            selects five or six faces and gathers -- then the level-lk cell.  Sign major:
+//            every wave but the one at the boundary has one sign (G_rand 5.40 -> 4.74 ms
+//            against cell major, where each cell's two signs alternate within a wave; the
+//            octant major over 8x coarser cells 4.79, sign major over them 4.85);
+//   specular the cone's aperture tau = clamp(roughness) in half octaves, then a cell 8x
+//            coarser than the diffuse one: the pixels of one aperture class are contiguous, so
+//            a wave's lanes share one tau (one step table, wave-uniform levels) and lie in
+//            Morton-adjacent cells.  A specular cone's mip level is log2(2 tau t): lanes whose tau
 //            differ by more than a fraction of an octave disagree on the level at most
 //            steps, and such a step is gathered per lane at per-lane levels (64-bit
 //            addresses, both levels one after the other).
@@ -51,13 +53,31 @@ namespace {
 
 // key kinds: cell bits and class bits (at most 2^22 counters = 16 MB)
 enum { kKeyDiffuse = 0, kKeySpecular = 1 };
-template <int KIND> constexpr uint32_t key_class_bits() { return KIND == kKeyDiffuse ? 1u : 4u; }
+// the diffuse key (A/B): 0 = the cell, then sign(n.z); 1 = sign(n.z), then the cell (default);
+// 2 = the normal's octant (signs of x, y, z), then the cell
+#ifndef VCT_DIFF_KEY_MODE
+#define VCT_DIFF_KEY_MODE 1
+#endif
+// the specular key's normal bits between the aperture class and the cell (A/B): 0 (default),
+// 1 = sign(n.z), 3 = the octant (G_rand 4.74 / 5.09 / 5.85 ms, the latter two over 15-bit cells)
+#ifndef VCT_SPEC_NRM_BITS
+#define VCT_SPEC_NRM_BITS 0
+#endif
+template <int KIND> constexpr uint32_t key_class_bits() {
+    return KIND == kKeyDiffuse ? (VCT_DIFF_KEY_MODE == 2 ? 3u : 1u) : 4u + VCT_SPEC_NRM_BITS;
+}
 #ifndef VCT_KEY_DIFF_BITS
 #define VCT_KEY_DIFF_BITS 21
 #endif
+// the specular key: aperture class major, then the level-lk cell (A/B switches; G_rand, ms per
+// frame, DESIGN 13.4: cell-major with 18 / 15 / 12 / 9 cell bits 6.46 / 5.96 / 6.08 / 6.91,
+// aperture-major with 15 / 18 cell bits 5.54 / 5.42 against cell-major 15 bits 5.54-5.59)
+#ifndef VCT_SPEC_TAU_MAJOR
+#define VCT_SPEC_TAU_MAJOR 1
+#endif
 #ifndef VCT_KEY_SPEC_BITS
-#define VCT_KEY_SPEC_BITS 15   // level-3 cells at 256^3 (measured on G_rand, ms per frame: 18 bits 6.46,
-#endif                         // 15 bits 5.96, 12 bits 6.08, 9 bits 6.91)
+#define VCT_KEY_SPEC_BITS 18
+#endif
 template <int KIND> constexpr uint32_t key_cell_bits() { return KIND == kKeyDiffuse ? VCT_KEY_DIFF_BITS : VCT_KEY_SPEC_BITS; }
 constexpr int kScanPer = 16;                // counters per thread in the scan kernels
 constexpr uint32_t kScanTile = 256u * kScanPer;
@@ -127,7 +147,17 @@ __global__ void __launch_bounds__(256) k_reorder_count(const float4* __restrict_
             return (uint32_t)(f < 0.0f ? 0 : (f > (float)(n - 1) ? n - 1 : (int)f)) >> lk;
         };
         c = spread3(q(ox)) | (spread3(q(oy)) << 1) | (spread3(q(oz)) << 2);
-        if (KIND == kKeyDiffuse) c = (c << 1) | (N.z < 0.0f ? 1u : 0u);
+        const uint32_t cbits = 3u * (uint32_t)(__builtin_ctz((uint32_t)n) - lk);
+        if (KIND == kKeyDiffuse) {
+            if (VCT_DIFF_KEY_MODE == 0) c = (c << 1) | (N.z < 0.0f ? 1u : 0u);
+            else if (VCT_DIFF_KEY_MODE == 1) c |= (N.z < 0.0f ? 1u : 0u) << cbits;
+            else c |= ((N.x < 0.0f ? 1u : 0u) | (N.y < 0.0f ? 2u : 0u) | (N.z < 0.0f ? 4u : 0u)) << cbits;
+        }
+        else if (VCT_SPEC_TAU_MAJOR) {
+            const uint32_t oct = (N.x < 0.0f ? 1u : 0u) | (N.y < 0.0f ? 2u : 0u) | (N.z < 0.0f ? 4u : 0u);
+            const uint32_t nb = VCT_SPEC_NRM_BITS == 3 ? oct : (VCT_SPEC_NRM_BITS == 1 ? oct >> 2 : 0u);
+            c |= ((tau_class(alb[i].w) << VCT_SPEC_NRM_BITS) | nb) << cbits;
+        }
         else c = (c << 4) | tau_class(alb[i].w);
         r = atomicAdd(cnt + c, 1u);
     }
@@ -206,6 +236,7 @@ static hipError_t sort_pixels(vct_ctx* c, const vct_trace_args* a, uint32_t* kv,
     const Grid& g = c->grid;
     const uint32_t npx = a->width * a->height;
     const uint32_t lgn = (uint32_t)__builtin_ctz(g.n);
+    static_assert(key_cell_bits<KIND>() + key_class_bits<KIND>() <= 22u, "counters: at most 2^22 + 1 (launch_reorder)");
     const uint32_t cb = key_cell_bits<KIND>();
     const uint32_t lk = 3u * lgn > cb ? (3u * lgn - cb + 2u) / 3u : 0u;   // cells: level-lk voxels
     const uint32_t ncell = 1u << (3u * (lgn - lk) + key_class_bits<KIND>());
