@@ -72,6 +72,12 @@ template <int KIND> constexpr uint32_t key_class_bits() {
 // the specular key: aperture class major, then the level-lk cell (A/B switches; G_rand, ms per
 // frame, DESIGN 13.4: cell-major with 18 / 15 / 12 / 9 cell bits 6.46 / 5.96 / 6.08 / 6.91,
 // aperture-major with 15 / 18 cell bits 5.54 / 5.42 against cell-major 15 bits 5.54-5.59)
+// super-cells of the class-major keys: the top 9 Morton bits (8^3 super-cells) above the class
+// (G_rand ms: class fully major 4.74, 3 / 6 / 9 / 12 / 15 bits 4.78-4.80 / 4.83 / 4.62-4.64 /
+// 4.70 / 5.0-5.2)
+#ifndef VCT_KEY_SUPER_BITS
+#define VCT_KEY_SUPER_BITS 9
+#endif
 #ifndef VCT_SPEC_TAU_MAJOR
 #define VCT_SPEC_TAU_MAJOR 1
 #endif
@@ -148,15 +154,21 @@ __global__ void __launch_bounds__(256) k_reorder_count(const float4* __restrict_
         };
         c = spread3(q(ox)) | (spread3(q(oy)) << 1) | (spread3(q(oz)) << 2);
         const uint32_t cbits = 3u * (uint32_t)(__builtin_ctz((uint32_t)n) - lk);
+        // class-major keys can keep the top VCT_KEY_SUPER_BITS Morton bits above the class
+        // (super-cells: each class is swept once per super-cell instead of once per grid)
+        const uint32_t lo = cbits > (uint32_t)VCT_KEY_SUPER_BITS ? cbits - (uint32_t)VCT_KEY_SUPER_BITS : 0u;
+        const auto cls = [c, lo](uint32_t k, uint32_t kb) {
+            return ((c >> lo) << (lo + kb)) | (k << lo) | (c & ((1u << lo) - 1u));
+        };
         if (KIND == kKeyDiffuse) {
             if (VCT_DIFF_KEY_MODE == 0) c = (c << 1) | (N.z < 0.0f ? 1u : 0u);
-            else if (VCT_DIFF_KEY_MODE == 1) c |= (N.z < 0.0f ? 1u : 0u) << cbits;
-            else c |= ((N.x < 0.0f ? 1u : 0u) | (N.y < 0.0f ? 2u : 0u) | (N.z < 0.0f ? 4u : 0u)) << cbits;
+            else if (VCT_DIFF_KEY_MODE == 1) c = cls(N.z < 0.0f ? 1u : 0u, 1u);
+            else c = cls((N.x < 0.0f ? 1u : 0u) | (N.y < 0.0f ? 2u : 0u) | (N.z < 0.0f ? 4u : 0u), 3u);
         }
         else if (VCT_SPEC_TAU_MAJOR) {
             const uint32_t oct = (N.x < 0.0f ? 1u : 0u) | (N.y < 0.0f ? 2u : 0u) | (N.z < 0.0f ? 4u : 0u);
             const uint32_t nb = VCT_SPEC_NRM_BITS == 3 ? oct : (VCT_SPEC_NRM_BITS == 1 ? oct >> 2 : 0u);
-            c |= ((tau_class(alb[i].w) << VCT_SPEC_NRM_BITS) | nb) << cbits;
+            c = cls((tau_class(alb[i].w) << VCT_SPEC_NRM_BITS) | nb, 4u + VCT_SPEC_NRM_BITS);
         }
         else c = (c << 4) | tau_class(alb[i].w);
         r = atomicAdd(cnt + c, 1u);
