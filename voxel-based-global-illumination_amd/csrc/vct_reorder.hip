@@ -60,11 +60,15 @@ enum { kKeyDiffuse = 0, kKeySpecular = 1 };
 #endif
 // the specular key's normal bits between the aperture class and the cell (A/B): 0 (default),
 // 1 = sign(n.z), 3 = the octant (G_rand 4.74 / 5.09 / 5.85 ms, the latter two over 15-bit cells)
+// aperture classes per octave: 2^(VCT_SPEC_TAU_BITS - 3) (4 bits: half octaves)
+#ifndef VCT_SPEC_TAU_BITS
+#define VCT_SPEC_TAU_BITS 4
+#endif
 #ifndef VCT_SPEC_NRM_BITS
 #define VCT_SPEC_NRM_BITS 0
 #endif
 template <int KIND> constexpr uint32_t key_class_bits() {
-    return KIND == kKeyDiffuse ? (VCT_DIFF_KEY_MODE == 2 ? 3u : 1u) : 4u + VCT_SPEC_NRM_BITS;
+    return KIND == kKeyDiffuse ? (VCT_DIFF_KEY_MODE == 2 ? 3u : 1u) : (uint32_t)VCT_SPEC_TAU_BITS + VCT_SPEC_NRM_BITS;
 }
 #ifndef VCT_KEY_DIFF_BITS
 #define VCT_KEY_DIFF_BITS 21
@@ -125,8 +129,9 @@ __device__ __forceinline__ uint32_t block_scan256(uint32_t v, uint32_t& total) {
 __device__ __forceinline__ uint32_t tau_class(float rough) {
     const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
     const int ex = (int)((__float_as_uint(tau) >> 23) & 0xffu) - 127;   // -6 .. 0
-    const int hc = 2 * (ex + 7) + (int)((__float_as_uint(tau) >> 22) & 1u);
-    return (uint32_t)min(max(hc, 0), 15);
+    constexpr int sub = VCT_SPEC_TAU_BITS - 3;                          // mantissa bits per octave
+    const int hc = (ex + 7) * (1 << sub) + (int)((__float_as_uint(tau) >> (23 - sub)) & ((1u << sub) - 1u));
+    return (uint32_t)min(max(hc, 0), (1 << VCT_SPEC_TAU_BITS) - 1);
 }
 
 // key of each pixel (cell of its cone origin: level-lk voxels in Morton order, then the
@@ -168,9 +173,9 @@ __global__ void __launch_bounds__(256) k_reorder_count(const float4* __restrict_
         else if (VCT_SPEC_TAU_MAJOR) {
             const uint32_t oct = (N.x < 0.0f ? 1u : 0u) | (N.y < 0.0f ? 2u : 0u) | (N.z < 0.0f ? 4u : 0u);
             const uint32_t nb = VCT_SPEC_NRM_BITS == 3 ? oct : (VCT_SPEC_NRM_BITS == 1 ? oct >> 2 : 0u);
-            c = cls((tau_class(alb[i].w) << VCT_SPEC_NRM_BITS) | nb, 4u + VCT_SPEC_NRM_BITS);
+            c = cls((tau_class(alb[i].w) << VCT_SPEC_NRM_BITS) | nb, (uint32_t)VCT_SPEC_TAU_BITS + VCT_SPEC_NRM_BITS);
         }
-        else c = (c << 4) | tau_class(alb[i].w);
+        else c = (c << VCT_SPEC_TAU_BITS) | tau_class(alb[i].w);
         r = atomicAdd(cnt + c, 1u);
     }
     // the background shares one counter: one atomic per wave
