@@ -25,7 +25,7 @@
 //            every wave but the one at the boundary has one sign (G_rand 5.40 -> 4.74 ms
 //            against cell major, where each cell's two signs alternate within a wave; the
 //            octant major over 8x coarser cells 4.79, sign major over them 4.85);
-//   specular the cone's aperture tau = clamp(roughness) in half octaves, then a cell 8x
+//   specular the cone's aperture tau = clamp(roughness) in quarter octaves, then a cell 64x
 //            coarser than the diffuse one: the pixels of one aperture class are contiguous, so
 //            a wave's lanes share one tau (one step table, wave-uniform levels) and lie in
 //            Morton-adjacent cells.  A specular cone's mip level is log2(2 tau t): lanes whose tau
@@ -60,9 +60,11 @@ enum { kKeyDiffuse = 0, kKeySpecular = 1 };
 #endif
 // the specular key's normal bits between the aperture class and the cell (A/B): 0 (default),
 // 1 = sign(n.z), 3 = the octant (G_rand 4.74 / 5.09 / 5.85 ms, the latter two over 15-bit cells)
-// aperture classes per octave: 2^(VCT_SPEC_TAU_BITS - 3) (4 bits: half octaves)
+// aperture classes per octave: 2^(VCT_SPEC_TAU_BITS - 3): quarter octaves (G_rand ms under
+// super-cells: half octaves over 18-bit cells 4.62-4.64, quarter / eighth octaves over 15-bit
+// cells 4.56-4.59 / 4.57, octaves over 18-bit cells 4.77)
 #ifndef VCT_SPEC_TAU_BITS
-#define VCT_SPEC_TAU_BITS 4
+#define VCT_SPEC_TAU_BITS 5
 #endif
 #ifndef VCT_SPEC_NRM_BITS
 #define VCT_SPEC_NRM_BITS 0
@@ -86,7 +88,7 @@ template <int KIND> constexpr uint32_t key_class_bits() {
 #define VCT_SPEC_TAU_MAJOR 1
 #endif
 #ifndef VCT_KEY_SPEC_BITS
-#define VCT_KEY_SPEC_BITS 18
+#define VCT_KEY_SPEC_BITS 15
 #endif
 template <int KIND> constexpr uint32_t key_cell_bits() { return KIND == kKeyDiffuse ? VCT_KEY_DIFF_BITS : VCT_KEY_SPEC_BITS; }
 constexpr int kScanPer = 16;                // counters per thread in the scan kernels
