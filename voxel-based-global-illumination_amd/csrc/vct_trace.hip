@@ -216,6 +216,10 @@ constexpr int kCh = 4;
 #define VCT_K4_CHOCC 2
 #endif
 constexpr int kChOcc = VCT_K4_CHOCC;
+// the union form stages five-face cones too (4 x 4 x 3 bricks)
+#ifndef VCT_K4_FIVE
+#define VCT_K4_FIVE 1
+#endif
 template <bool UNION> constexpr int gather_chunk() { return UNION ? kCh : kChOcc; }
 
 // trilinear corner weights (x fastest), w_c = (wx * wy) * wz
@@ -504,11 +508,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 struct ConeCtl {                 // wave-uniform facts about one cone
     int funion;                  // faces (bit per VCT_FACE_*) any valid lane selects
     int nfaces;                  // popcount(funion)
-    int f0, f1, f2, f3;          // the faces of funion in increasing order (first nfaces valid)
+    int f0, f1, f2, f3, f4;      // the faces of funion in increasing order (first nfaces valid)
     bool dir_uniform;            // every valid lane has the same wd = d^2 (bitwise) and the same faces
     int neg;                     // bit a: every valid lane moves toward -axis a (brick slack goes there)
     float uwx, uwy, uwz;         // that wd
-    int z3;                      // 1: faces-mode bricks are 4 x 4 x 3 (a four-face cone in the occupancy form)
+    int z3;                      // 1: faces-mode bricks are 4 x 4 x 3 (a four-face cone in the occupancy form,
+                                 // a five-face cone in the union form)
     int bstr;                    // faces-mode block stride (kBlk, or kBlk3 with z3)
 };
 
@@ -672,6 +677,28 @@ __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const T
     return nz == 0u;
 }
 
+// the fifth face block of a five-face brick (union form, 4 x 4 x 3): face f4 at block 4,
+// staged after the other four (its texel is not held with them: the union form has no
+// VGPRs to spare); true when the lane stored +0 only
+template <bool O32>
+__device__ __forceinline__ bool stage_face5(const TraceK& k, int l, const BrickEntry& be, const ConeCtl& cc,
+                                            float4* __restrict__ lds) {
+    const int nl = k.n >> l;
+    const int lane = lane_id_opaque();
+    const int sx = be.ox + (lane & 3), sy = be.oy + ((lane >> 2) & 3), sz = be.oz + (lane >> 4);
+    const bool inb = (unsigned)sx < (unsigned)nl && (unsigned)sy < (unsigned)nl && (unsigned)sz < (unsigned)nl;
+    const uint32_t gi = texel_index_lg((uint32_t)sx, (uint32_t)sy, (uint32_t)sz, (uint32_t)(k.lgn - l));
+    const LevelView<O32> lv = level_view<O32>(k, l);
+    const uint32_t sh = 3u * (uint32_t)(k.lgn - l);
+    const float4 v = lv.fetch(((uint32_t)cc.f4 << sh) + gi, inb);
+    uint32_t nz = 0u;
+    if (lane < 48) {
+        lds[(lane & 15) + kBz * (lane >> 4) + 4 * kBlk3] = v;
+        nz = bits4(v);
+    }
+    return nz == 0u;
+}
+
 // slot of the lane's corner 0 in a staged entry
 __device__ __forceinline__ int brick_slot(const Corner& c, const BrickEntry& be) {
     return (c.ix - be.ox) + 4 * (c.iy - be.oy) + __mul24(kBz, c.iz - be.oz);
@@ -732,16 +759,16 @@ __device__ __forceinline__ void dbg_fallback_reason(const Corner& c, bool active
 // derivations back out of the loop (a few VALU in the faces-mode / gather paths only).
 struct LaneDir {
     float dx, dy, dz;
-    uint32_t blk;                // bits 0-1 / 2-3 / 4-5: the x / y / z face's block index in the union
+    uint32_t blk;                // bits 0-2 / 3-5 / 6-8: the x / y / z face's block index in the union
     __device__ int fx() const { return dx >= 0.0f ? VCT_FACE_PX : VCT_FACE_NX; }
     __device__ int fy() const { return dy >= 0.0f ? VCT_FACE_PY : VCT_FACE_NY; }
     __device__ int fz() const { return dz >= 0.0f ? VCT_FACE_PZ : VCT_FACE_NZ; }
     __device__ float wx() const { return dx * dx; }
     __device__ float wy() const { return dy * dy; }
     __device__ float wz() const { return dz * dz; }
-    __device__ int bx(int str) const { return __mul24(str, (int)(blk & 3u)); }
-    __device__ int by(int str) const { return __mul24(str, (int)((blk >> 2) & 3u)); }
-    __device__ int bz(int str) const { return __mul24(str, (int)(blk >> 4)); }
+    __device__ int bx(int str) const { return __mul24(str, (int)(blk & 7u)); }
+    __device__ int by(int str) const { return __mul24(str, (int)((blk >> 3) & 7u)); }
+    __device__ int bz(int str) const { return __mul24(str, (int)(blk >> 6)); }
 };
 
 // One step's blended sample (1 - fr) D_{l0} + fr D_{l0+1} for a wave-uniform l0.
@@ -762,7 +789,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const int aniso_mode = AM >= 0 ? AM : (cc.dir_uniform ? kComb : kFaces);
     const int modeA = (l0 == 0 || !k.aniso) ? kIso : aniso_mode;
     const int modeB = k.aniso ? aniso_mode : kIso;
-    const bool faces_ok = AM == kComb || cc.nfaces <= 4;
+    const bool faces_ok = AM == kComb || cc.nfaces <= (UNION && VCT_K4_FIVE ? 5 : 4);
     // faces-mode levels of a four-face cone in the occupancy form: 4 x 4 x 3 bricks
     // (a dir_uniform cone has three faces: never z3)
     const int z3A = AM != kComb && modeA == kFaces ? cc.z3 : 0, z3B = AM != kComb && modeB == kFaces ? cc.z3 : 0;
@@ -815,7 +842,11 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // a brick whose texels are all +0 (empty space) is marked: its samples are exactly
     // zero (fmaf(w, +0, +0) = +0 through the whole trilinear chain), so hits on it skip
     // the LDS reads and the FMAs
-    if (stB) bB.zero = bc.b.zero = wall(stage_store<AM>(modeB, cc, tB, ldsB));
+    if (stB) {
+        bool zB = stage_store<AM>(modeB, cc, tB, ldsB);
+        if (UNION && VCT_K4_FIVE && AM != kComb && modeB == kFaces && cc.nfaces > 4) zB = stage_face5<O32>(k, l1, bB, cc, ldsB) && zB;
+        bB.zero = bc.b.zero = wall(zB);
+    }
     bool stA = false;
     if (!useA && !emptyA && (modeA != kFaces || faces_okA)) {
         BrickEntry nb{};
@@ -831,7 +862,11 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     if (useA && modeA == kFaces) VCT_DBG(29);               // brick samples read three faces per corner
     if (useB && modeB == kFaces) VCT_DBG(30);
     pc.mark(1);
-    if (stA) bA.zero = bc.a.zero = wall(stage_store<AM>(modeA, cc, stage_load<O32, AM>(k, l0, bA, modeA, cc), ldsA));
+    if (stA) {
+        bool zA = stage_store<AM>(modeA, cc, stage_load<O32, AM>(k, l0, bA, modeA, cc), ldsA);
+        if (UNION && VCT_K4_FIVE && AM != kComb && modeA == kFaces && cc.nfaces > 4) zA = stage_face5<O32>(k, l0, bA, cc, ldsA) && zA;
+        bA.zero = bc.a.zero = wall(zA);
+    }
     if (stA || stB) wave_lds_sync();
     pc.mark(2);
     float4 sA = z4, sB = z4;
@@ -969,18 +1004,21 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.f2 = __builtin_ctz(u | 64);
         u &= u - 1;
         cc.f3 = __builtin_ctz(u | 64);
+        u &= u - 1;
+        cc.f4 = __builtin_ctz(u | 64);
         // a background lane's faces may lie outside the union (which only the valid lanes
         // define): it gets block 0, so its (discarded) brick samples read staged texels
         ld.blk = valid ? (uint32_t)__builtin_popcount(cc.funion & ((1 << fx) - 1)) |
-                             (uint32_t)__builtin_popcount(cc.funion & ((1 << fy) - 1)) << 2 |
-                             (uint32_t)__builtin_popcount(cc.funion & ((1 << fz) - 1)) << 4
+                             (uint32_t)__builtin_popcount(cc.funion & ((1 << fy) - 1)) << 3 |
+                             (uint32_t)__builtin_popcount(cc.funion & ((1 << fz) - 1)) << 6
                        : 0u;
         cc.uwx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdx), fl));
         cc.uwy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdy), fl));
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
         // same d^2 everywhere AND one face per axis (d and -d share d^2)
         cc.dir_uniform = wall_in(vm, (wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz)) && cc.nfaces == 3;
-        cc.z3 = !UNION && cc.nfaces == 4 ? 1 : 0;
+        // the union form's 292-slot entries hold five 4 x 4 x 3 face blocks (270 slots)
+        cc.z3 = (!UNION && cc.nfaces == 4) || (UNION && VCT_K4_FIVE && cc.nfaces == 5) ? 1 : 0;
         cc.bstr = cc.z3 ? kBlk3 : kBlk;
     }
     BrickCache bc;
