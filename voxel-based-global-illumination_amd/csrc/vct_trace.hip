@@ -1367,8 +1367,10 @@ __global__ void __launch_bounds__(64, MINW) k4_trace(TraceK k) {
 // Each unit's duration is read once (a concurrent frame may be rewriting it: any values
 // give a permutation), so the result is always a permutation of the units and the frame's
 // outputs are those of blockIdx order (every unit runs the same arithmetic wherever it is
-// dispatched).  Measured (tools/lpt_emul.py, same-frame durations): one rank of 8 at 1080p
-// 0.234 -> 0.201 ms, one of 4 0.392 -> 0.364 ms, the full C3 frame 1.109 -> 1.073 ms.
+// dispatched).  Emulated (tools/lpt_emul.py, same-frame durations): one rank of 8 at 1080p
+// 0.234 -> 0.201 ms, one of 4 0.392 -> 0.364 ms, the full C3 frame 1.109 -> 1.073 ms; on the
+// device the full frame lost (the order kernel and the scattered tiles cost more than its
+// tail), hence launch_trace's size and overlap rule.
 constexpr uint32_t kLptMaxGenerations = 4;       // LPT for launches of <= 4 x (CUs x 20) waves
 constexpr uint32_t kLptBuckets = 128;
 constexpr uint32_t kLptMaxPerClass = 48u * 1024u;   // key bytes per class in LDS
