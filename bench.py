@@ -207,6 +207,12 @@ def roofline(rec, reason, k4_ms, texels, valid_px, profile_path, key, steps=None
     out = {"bound": "issue (VALU)", "achieved": None, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s", "frac": None,
            "traffic": None, "gather_bytes": gather,
            "gather_GBs": round(gather / (k4_ms * 1e-3) / 1e9, 1) if gather is not None and k4_ms else None,
+           # north_star's "% of HBM roofline": SURVEY 8d's algorithmic bytes over the live K4 time
+           # against 8 TB/s.  Above 1 because the gathered texels come from LDS bricks and L2,
+           # not HBM (the 60 % HBM target cannot describe an on-chip gather); the
+           # counter HBM fraction is "hbm" below, the binding resource "bound"
+           "hbm_algorithmic_frac": round(gather / (k4_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 3)
+           if gather is not None and k4_ms else None,
            "texel_fetches_per_launch": texels, "k4_ms": round(k4_ms, 4) if k4_ms else None,
            "peak_basis": "1024 SIMD-32 x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
     if rec is None or not k4_ms:
@@ -668,6 +674,10 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
                        variant=args.variant)
     torch.cuda.synchronize()
     local_steps, local_texels = int(cnt[0].item()), int(cnt[1].item())
+    # the counting frame's planes: the timed frames (another compiled form, no counters,
+    # perhaps reordered or dispatched longest first) must equal them bit for bit
+    lp = tracer.local_planes(0)
+    counted = None if lp is None else (lp[0].clone(), lp[1].clone())
     valid = (gb[0][..., 3] != 0).reshape(-1).cpu().numpy()
     fi, _ = compact_index(w, h, rank, world)
     local_valid = int(valid[fi].sum())
@@ -699,6 +709,10 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(torch, dist, dev, [elapsed], world)[0]
     progress(rank, f"  {scene_name}: {args.steps} timed frames done")
+    lp = tracer.local_planes(tracer.last_buf)       # the last timed frame (drained above)
+    same = counted is None or (torch.equal(lp[0], counted[0]) and torch.equal(lp[1], counted[1]))
+    timed_equals_counting = max_over_ranks(torch, dist, dev, [0.0 if same else 1.0], world)[0] == 0.0
+    del counted
     k4_ov_ms = [a.elapsed_time(b) for a, b in ev]
     # K4 alone (the roofline's launch duration): K frames back to back on the ctx stream,
     # no other work on the GPU -- in the pipelined loop consecutive traces share the chip
@@ -720,7 +734,7 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
         "frame_relight_ms": round(min(k2_ms + bcast_ms + k3_ms, k2_rep_ms + k3_rep_ms) + ms_per_step, 3),
         "frame_relight_bcast_ms": round(k2_ms + bcast_ms + k3_ms + ms_per_step, 3),
         "frame_relight_replicated_ms": round(k2_rep_ms + k3_rep_ms + ms_per_step, 3),
-        "replicated_k2_equals_bcast": k2_rep_match,
+        "replicated_k2_equals_bcast": k2_rep_match, "timed_equals_counting": timed_equals_counting,
         "_gb": gb, "_eye": eye, "_steps_px": steps_px,
     })
     if world > 1:
@@ -750,7 +764,7 @@ def form_name(f):
     """vct_trace_form -> its description (None while timing)"""
     if f is None or f < 0:
         return None
-    return ("occupancy, 5 waves/SIMD" if f & 1 else "four-face union, 4 waves/SIMD") + (
+    return ("occupancy, 5 waves/SIMD" if f & 1 else "union (bricks of up to five faces), 4 waves/SIMD") + (
         ", ray reordering" if f & 2 else ", screen order")
 
 
@@ -840,8 +854,9 @@ def measure_config(args, torch, dist, rank, world, dev, stream, cfg):
            "k4_form_rank0": form_name(m["k4_form"]), "overlap_tune_rank0": m["overlap_tune"],
            "value_single_launch": round(m["frame_cone_steps"] / m["k4_kernel_ms_avg"] / 1e3, 2) if world == 1 else None,
            "roofline_rank0": roof}
-    for k_ in ("k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "k3_mips_relight_ms", "grid_bcast_ms", "frame_relight_ms",
-               "replicated_k2_equals_bcast", "trace_ms_max_rank", "gather_ms", "allgather_ms"):
+    for k_ in ("timed_equals_counting", "k1_voxelize_ms", "k2_inject_ms", "k3_mips_ms", "k3_mips_relight_ms",
+               "grid_bcast_ms", "frame_relight_ms", "replicated_k2_equals_bcast", "trace_ms_max_rank", "gather_ms",
+               "allgather_ms"):
         if k_ in m:
             out[k_] = m[k_]
     if world > 1:
@@ -934,6 +949,7 @@ def stress_rand(args, torch, ctx, dev, stream):
         sp = torch.empty((h, w, 4), device=dev)
         if v & 0x4000000:      # the counting pass, once (screen order)
             ctx.trace_device(*gb, w, h, eye, d, sp, cone_steps=cnt, variant=v)
+            counted = (d.clone(), sp.clone())
         # a forced order holds at once; the default variant may first re-time the choice it made
         # on G_scene under the same workload key (drift watch), so it settles longer
         form[v] = settle_form(ctx, torch, lambda: ctx.trace_device(*gb, w, h, eye, d, sp, variant=v),
@@ -966,7 +982,9 @@ def stress_rand(args, torch, ctx, dev, stream):
             "speedup": round(t0 / t1, 3), "k4_forms": list(form.values()),
             "default_choice": "ray reordering" if form[auto] >= 0 and form[auto] & 2 else "screen order",
             "bitexact": bool(torch.equal(a0, b0) and torch.equal(a1, b1) and torch.equal(a0, c0) and
-                             torch.equal(a1, c1))}
+                             torch.equal(a1, c1)),
+            "timed_equals_counting": bool(all(torch.equal(x, counted[0]) and torch.equal(y, counted[1])
+                                              for x, y in outs.values()))}
 
 
 def run(args, world):
@@ -1062,6 +1080,7 @@ def run(args, world):
         result["frame_overlap"] = "two trace streams" if m["overlap"] else "one stream"
         result["overlap_tune"] = m["overlap_tune"]
         result["k4_form"] = form_name(m["k4_form"])
+        result["timed_equals_counting"] = m["timed_equals_counting"]
         # (the timed loops here overlap frames or follow overlapped ones: blockIdx order)
         result["k4_dispatch"] = ("blockIdx order through the XCD map; each XCD's units longest first (from the "
                                  "previous launch's per-unit wave durations) only in launches of <= 4 generations of "
@@ -1129,6 +1148,7 @@ def run(args, world):
                 "ms_per_step": round(s2["ms_per_step"], 4), "k4_kernel_ms_avg": round(s2["k4_kernel_ms_avg"], 4),
                 "frame_cone_steps": s2["frame_cone_steps"], "valid_px": s2["valid_px"],
                 "k1_voxelize_ms": s2["k1_voxelize_ms"], "k4_form": form_name(s2["k4_form"]),
+                "timed_equals_counting": s2["timed_equals_counting"],
                 "value_single_launch": round(s2["frame_cone_steps"] / s2["k4_kernel_ms_avg"] / 1e3, 2)
                 if world == 1 else None,
             }

@@ -381,7 +381,10 @@ vct_status vct_download_accum(vct_ctx* ctx, int64_t* sums6, uint32_t* counts);
  * Save needs the state a section comes from (VCT_ESTATE otherwise).  Load first checks
  * the payload's length and sha256 and that the dump's grid (n, aabb_min, extent, aniso)
  * is the context's, bit for bit (VCT_EINVAL otherwise, nothing changed); then it
- * replaces the context's grid state.  Synchronous. */
+ * replaces the context's grid state.  A failure after that point (a short or corrupt
+ * section, an upload or mips error, a rebuilt pyramid that differs) leaves the grid
+ * invalid: it reads as never voxelized (VCT_ESTATE for inject / mips / trace) until the
+ * next voxelization or successful load.  Synchronous. */
 #define VCT_DUMP_VOXELS  0x1u
 #define VCT_DUMP_LEVEL0  0x2u
 #define VCT_DUMP_PYRAMID 0x4u

@@ -739,6 +739,7 @@ vct_status vct_load_grid(vct_ctx* c, const char* stem) {
     uint32_t *idx = NULL, *cnt = NULL;
     int64_t* sums = NULL;
     float *buf = NULL, *pyr = NULL;
+    int mutated = 0;    /* a failure after the grid began to change leaves it invalid (vct.h) */
     if (vdump_check_config(&h, &c->cfg, err, sizeof err)) { st = fail(c, VCT_EINVAL, err); goto done; }
     if ((h.what & VCT_DUMP_PYRAMID) && !(h.what & VCT_DUMP_LEVEL0)) {
         st = fail(c, VCT_EINVAL, "load_grid: a pyramid section without level 0");
@@ -757,6 +758,7 @@ vct_status vct_load_grid(vct_ctx* c, const char* stem) {
                 st = fail(c, VCT_EINVAL, "load_grid: voxel section is not ascending in-range occupied voxels");
                 goto done;
             }
+        mutated = 1;
         memset(c->sums, 0, nv * 6 * sizeof(int64_t));
         memset(c->counts, 0, nv * sizeof(uint32_t));
         for (size_t i = 0; i < occ; ++i) {
@@ -773,6 +775,7 @@ vct_status vct_load_grid(vct_ctx* c, const char* stem) {
         buf = (float*)malloc(nv * 16);
         if (!buf) { st = fail(c, VCT_ENOMEM, "load_grid: host memory"); goto done; }
         if (vdump_read(&r, buf, nv * 16, err, sizeof err)) { st = fail(c, VCT_EINVAL, err); goto done; }
+        mutated = 1;
         if ((st = vct_upload_level0(c, buf)) != VCT_OK || (st = vct_build_mips(c)) != VCT_OK) goto done;
         if (h.what & VCT_DUMP_PYRAMID) {
             const size_t pf = vo_pyramid_floats(c->n, c->aniso);   /* levels 1..L */
@@ -784,6 +787,7 @@ vct_status vct_load_grid(vct_ctx* c, const char* stem) {
         }
     }
 done:
+    if (st != VCT_OK && mutated) c->voxelized = c->injected = c->mipped = 0;
     vdump_close(&r);
     free(idx); free(cnt); free(sums); free(buf); free(pyr);
     return st;

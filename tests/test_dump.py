@@ -201,6 +201,57 @@ def test_grid_dump_damage_refused(cpu_lib, tmp_path):
         x.close()
 
 
+def _failing_pyramid_dump(ctx, tmp_path):
+    """A dump whose payload is intact (length and sha256 re-stamped) but whose last pyramid
+    texel differs from the rebuilt one: refused only after the grid began to change."""
+    import hashlib
+    import json
+    from vct import dump
+    dump.save_grid(ctx, tmp_path / "f", pyramid=True)
+    raw = bytearray((tmp_path / "f.bin").read_bytes())
+    raw[-2] ^= 0x40                     # an exponent bit of the last float of the top level
+    (tmp_path / "f.bin").write_bytes(bytes(raw))
+    hdr = json.loads((tmp_path / "f.json").read_text())
+    hdr["sha256"] = hashlib.sha256(bytes(raw)).hexdigest()
+    (tmp_path / "f.json").write_text(json.dumps(hdr))
+    return tmp_path / "f"
+
+
+def _assert_load_fails_invalid(lib, tmp_path, n, name):
+    """a load that fails after the header checks leaves no half-loaded grid:
+    inject, mips and trace refuse the context (VCT_ESTATE) until a new voxelization."""
+    from helpers import scene_arrays
+    from vct import VctError, dump, scenes
+    src = _grid(lib, n=n, name=name)
+    bad = _failing_pyramid_dump(src, tmp_path)
+    dst = _grid(lib, n=n, name=name, light=LIGHT2)
+    with pytest.raises(ValueError, match="differ"):
+        dump.load_grid(bad, ctx=dst)
+    pos, nrm, alb, eye = _gbuf(n)
+    with pytest.raises(VctError, match="ESTATE"):
+        dst.trace(pos, nrm, alb, eye)
+    with pytest.raises(VctError, match="ESTATE"):
+        dst.build_mips()
+    with pytest.raises(VctError, match="ESTATE"):
+        dst.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    _, (v, i, m, k) = scene_arrays(name)     # a new voxelization makes it usable again
+    dst.voxelize(v, i, m, k)
+    dst.inject_directional(scenes.LIGHT_DIR, scenes.LIGHT_COLOR)
+    dst.build_mips()
+    _same_frames(src, dst, _gbuf(n))
+    src.close()
+    dst.close()
+
+
+def test_grid_dump_failed_load_invalidates_cpu(cpu_lib, tmp_path):
+    _assert_load_fails_invalid(cpu_lib, tmp_path, 16, "cornell")
+
+
+@pytest.mark.gpu
+def test_grid_dump_failed_load_invalidates_gpu(gpu_ready, tmp_path):
+    _assert_load_fails_invalid(None, tmp_path, 32, "cornell")
+
+
 def test_sha256_matches_hashlib(cpu_lib, tmp_path):
     """The C SHA-256 of vct_dumpio.c (the header's payload hash) is hashlib's."""
     import hashlib

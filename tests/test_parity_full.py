@@ -19,10 +19,17 @@ cone-step counter equals the sum of its per-pixel counts, a second launch is
 bit-identical, and the multi-GPU screen-tile partition (2/4/8 ranks, traced on
 this one device) reproduces the single-rank frame bit for bit.
 
+Every TIMED form of K4 is run at these sizes too, counter-free as the bench times
+it: the union and the occupancy form, each in screen order and with ray
+reordering (forced by variant bits), the default workload after the tuner has
+settled, and the 2/4/8-rank tiles with both forms forced and after settling (the
+small launches of 8 ranks then run in longest-first order).
+
 G-buffers come from the HIP tile-binned G-buffer pass (row f2), which is
 bit-identical to the brute-force caster (test_parity_gpu.py); they are the
 input here, not the thing checked.
 """
+import ctypes as C
 import gc
 
 import numpy as np
@@ -33,6 +40,10 @@ from helpers import rel_l2
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
 TRACE_TOL = 1e-3   # north_star: indirect-irradiance parity within 1e-3 relative L2 (fp32)
+# forced K4 candidates (include/vct.h VCT_VARIANT_*) -> vct_trace_form (bit 0 occupancy form,
+# bit 1 ray reordering): union / occupancy in screen order, each with reordering
+FORCED_FORMS = {0x1000000 | 0x4000000: 0, 0x2000000 | 0x4000000: 1, 0x1000000 | 0x8000: 2, 0x2000000 | 0x8000: 3}
+SETTLE_LAUNCHES = 40   # > 4 candidates x (1 cold + 2 timed samples), then recorded and reordered launches
 
 CONFIGS = [
     # id, scene, n, w, h, n_diffuse, specular
@@ -133,18 +144,44 @@ def test_full_config_parity(gpu_ready, oracle_mod, cid, name, n, w, h, nd, spec)
     ctx.trace_device(*gb, w, h, cam.position, d2, sp2)
     torch.cuda.synchronize()
     assert torch.equal(d2, d) and torch.equal(sp2, sp)
-    # multi-GPU screen tiles: every rank's compact tiles un-permuted == the frame
+    # every timed form at this size: a fresh workload's first launches
+    # run the union form, so the occupancy form -- the headline's settled kernel at C3/C4 --
+    # and ray reordering are forced here, each counter-free, each against the oracle's frame
+    for variant in FORCED_FORMS:
+        d2.fill_(-1.0)
+        sp2.fill_(-1.0)
+        ctx.trace_device(*gb, w, h, cam.position, d2, sp2, variant=variant)
+        torch.cuda.synchronize()
+        assert ctx.trace_form == FORCED_FORMS[variant], (cid, hex(variant), ctx.trace_form)
+        assert torch.equal(d2, d) and torch.equal(sp2, sp), f"{cid}: forced form {variant:#x} differs"
+    # ... and the default workload once its choice has settled: the timed launches of a
+    # renderer (and of bench.py's loop) run whichever form / order the tuner kept
+    for _ in range(SETTLE_LAUNCHES):
+        ctx.trace_device(*gb, w, h, cam.position, d2, sp2)
+    torch.cuda.synchronize()
+    assert ctx.trace_form >= 0, f"{cid}: tuner did not settle"
+    assert torch.equal(d2, d) and torch.equal(sp2, sp), f"{cid}: settled form {ctx.trace_form} differs"
+    # multi-GPU screen tiles: every rank's compact tiles un-permuted == the frame, for both
+    # forms forced and for the settled default (small launches: longest-first dispatch)
     from vct.multi import tiles_for_rank
+    lpt = ctx.lib.vct_debug_k4_lpt_launches
+    lpt.restype, lpt.argtypes = C.c_longlong, [C.c_void_p]
     for world in (2, 4, 8):
         maxt = tiles_for_rank(w, h, 0, world)
         g = torch.zeros((world, 2, maxt * 4096, 4), device=dev)
-        for r in range(world):
-            ctx.trace_device(*gb, w, h, cam.position, g[r, 0], g[r, 1], tile_rank=r, tile_world=world,
-                             tile_compact=True)
-        fd, fs = torch.zeros_like(d), torch.zeros_like(sp)
-        ctx.untile_planes_device(g, w, h, world, (fd, fs))
-        torch.cuda.synchronize()
-        assert torch.equal(fd, d) and torch.equal(fs, sp), f"{cid}: {world}-rank tiles differ"
+        for variant in (0x1000000, 0x2000000, 0):
+            g.fill_(-1.0)
+            before = lpt(ctx.h)
+            for r in range(world):
+                for _ in range(SETTLE_LAUNCHES if variant == 0 else 1):
+                    ctx.trace_device(*gb, w, h, cam.position, g[r, 0], g[r, 1], tile_rank=r, tile_world=world,
+                                     tile_compact=True, variant=variant)
+            fd, fs = torch.zeros_like(d), torch.zeros_like(sp)
+            ctx.untile_planes_device(g, w, h, world, (fd, fs))
+            torch.cuda.synchronize()
+            assert torch.equal(fd, d) and torch.equal(fs, sp), f"{cid}: {world}-rank tiles differ ({variant:#x})"
+            if variant == 0 and world == 8 and w * h <= 1920 * 1080:   # 4K ranks of 8 exceed kLptMaxGenerations
+                assert lpt(ctx.h) > before, f"{cid}: no 8-rank launch was dispatched longest first"
         del g
     print(f"{cid}: {name} {n}^3 {w}x{h} nd={nd} spec={spec}: occupied={occupied} valid_px={valid} "
           f"cone_steps={int(cnt.item())} rel_l2={both:.1e}")

@@ -6,6 +6,8 @@ integer / fixed-order float work -> BIT-EXACT.  K4 cone tracing: relative L2
 and the oracle share the spec's operation order, so the observed error is
 expected to be 0 and the per-pixel step counts identical.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -1386,12 +1388,16 @@ def test_trace_form_forced_reports_candidate(gpu_ready):
 
 @pytest.mark.parametrize("world,rank,gbuf", [(1, 0, "scene"), (8, 3, "scene"), (3, 1, "scene"), (1, 0, "rand")])
 def test_longest_first_dispatch_bitexact(gpu_ready, oracle_mod, world, rank, gbuf):
-    """Longest-first dispatch (vct_trace.hip k4_lpt_order): once a workload's candidate is
-    settled, every timed launch records each unit's wave duration and the next one deals
-    each XCD's units longest first.  Every launch -- the recording ones, the reordered ones
-    on one stream and, forced by 0x10000000, on two alternating streams (whose order tables
-    are per stream while the durations are shared), and with the dispatch off (0x20000000) -- equals the
-    counting launch bit for bit; so does the oracle's frame."""
+    """Longest-first dispatch (vct_trace.hip k4_lpt_bands / k4_lpt_order): once a workload's
+    candidate is settled, every timed launch records each unit's wave duration and the next
+    one deals each XCD's units longest first.  Every launch equals the counting launch bit
+    for bit, and so does the oracle's frame:
+    * the recording ones and the longest-first ones on one stream (the hook
+      vct_debug_k4_lpt_launches shows that an order table was applied);
+    * launches alternating between two streams, also with 0x10000000: these overlap
+      another frame, so they keep blockIdx order (the order scratch is shared by the
+      streams; the hook's count must not move);
+    * the dispatch switched off (0x20000000)."""
     import torch
     from vct.multi import TILE, tiles_for_rank
     n, w, h = 64, 320, 192
@@ -1423,13 +1429,19 @@ def test_longest_first_dispatch_bitexact(gpu_ready, oracle_mod, world, rank, gbu
         ref = oracle_mod.trace(n, g0, E, ctx.download_level(0), gpu_pyramid_flat(ctx), pos, nrm, alb, cam.position)
         assert np.array_equal(rd.reshape(h, w, 4), ref["diffuse"]) and np.array_equal(rs.reshape(h, w, 4), ref["spec"])
         assert steps == ref["cone_steps"]
+    lpt = ctx.lib.vct_debug_k4_lpt_launches
+    lpt.restype, lpt.argtypes = C.c_longlong, [C.c_void_p]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    for i in range(48):   # settle the candidate, record, then longest-first launches
-        stream = streams[i % 2] if i >= 32 else None
-        # overlapped launches dispatch longest first only when 0x10000000 asks for it
-        d, sp, _ = run(variant=0x10000000 if i >= 32 else 0, stream=stream)
-        assert np.array_equal(d, rd) and np.array_equal(sp, rs), (i, stream is not None)
+    for i in range(32):   # settle the candidate, record, then longest-first launches
+        d, sp, _ = run()
+        assert np.array_equal(d, rd) and np.array_equal(sp, rs), i
     assert ctx.trace_form >= 0
+    applied = lpt(ctx.h)
+    assert applied > 0, "no launch was dispatched longest first"
+    for i in range(16):   # two streams: never longest first, 0x10000000 or not
+        d, sp, _ = run(variant=0x10000000 if i % 4 < 2 else 0, stream=streams[i % 2])
+        assert np.array_equal(d, rd) and np.array_equal(sp, rs), ("two streams", i)
+    assert lpt(ctx.h) == applied
     d, sp, _ = run(variant=0x20000000)
     assert np.array_equal(d, rd) and np.array_equal(sp, rs)
     ctx.close()

@@ -132,8 +132,24 @@ vct_status vct_save_grid(vct_ctx* c, const char* stem, uint32_t what) {
     return VCT_OK;
 }
 
+// A load that fails after it began to replace the grid leaves no half-loaded state behind:
+// the grid reads as never voxelized (every trace, inject and mips call refuses it with
+// VCT_ESTATE until the next voxelization or load).
+struct InvalidateOnFail {
+    vct_ctx* c;
+    bool armed = false;
+    ~InvalidateOnFail() {
+        if (!armed) return;
+        Grid& g = c->grid;
+        g.voxelized = g.injected = g.mipped = false;
+        g.k2_coarse_ok = g.k3_sparse_ok = g.zm_valid = false;
+        ++c->grid_epoch;
+    }
+};
+
 vct_status vct_load_grid(vct_ctx* c, const char* stem) {
     if (!c || !stem) return VCT_EINVAL;
+    InvalidateOnFail guard{c};
     vdump_file r;
     char err[1024];
     if (vdump_open_read(&r, stem, err, sizeof err)) return dfail(c, VCT_EINVAL, std::string("load_grid: ") + err);
@@ -169,6 +185,7 @@ vct_status vct_load_grid(vct_ctx* c, const char* stem) {
             VCT_DHIP(hipMemcpyAsync(dr.p, rec.data(), occ * 56, hipMemcpyHostToDevice, c->stream), "upload");
         }
         // what a voxelization invalidates (voxelize_dev), then K1's state written back
+        guard.armed = true;
         g.voxelized = g.injected = g.mipped = false;
         g.k2_coarse_ok = g.k3_sparse_ok = g.zm_valid = false;
         g.k3_live_bz = 0;
@@ -183,6 +200,7 @@ vct_status vct_load_grid(vct_ctx* c, const char* stem) {
     if (h.what & VCT_DUMP_LEVEL0) {
         std::vector<float> buf(nv * 4), mine(nv * 4);
         if (vdump_read(&r, buf.data(), nv * 16, err, sizeof err)) return dfail(c, VCT_EINVAL, std::string("load_grid: ") + err);
+        guard.armed = true;
         vct_status st = vct_upload_level0(c, buf.data());
         if (st == VCT_OK) st = vct_build_mips(c);
         if (st != VCT_OK) return st;
@@ -199,6 +217,7 @@ vct_status vct_load_grid(vct_ctx* c, const char* stem) {
             }
         }
     }
+    guard.armed = false;
     return VCT_OK;
 }
 

@@ -199,6 +199,7 @@ struct vct_ctx {
     vct::StepRow* spec_rows = nullptr;  // [kSpecSlots][64] specular step tables (filled by K4)
     const uint32_t* k4_dbg_order = nullptr;   // vct_debug_k4_sched (tools): K4 dispatch order
     uint32_t* k4_dbg_dur = nullptr;           // and per-unit wave durations
+    uint64_t k4_lpt_launches = 0;             // launches dispatched longest first (vct_debug_k4_lpt_launches)
     int* k1_err = nullptr;              // device flag of vct_voxelize_device (index out of range)
     // vct_create_multi: this context is device rank 0 and owns one context per
     // further device (ranks 1..n-1); empty for a single-device context

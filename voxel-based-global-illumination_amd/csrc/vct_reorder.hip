@@ -127,7 +127,8 @@ __device__ __forceinline__ uint32_t block_scan256(uint32_t v, uint32_t& total) {
 }
 
 // aperture class of a specular cone: tau = clamp(roughness, VCT_SPEC_TAU_MIN, VCT_SPEC_TAU_MAX)
-// (as K4 computes it) in half octaves, from its exponent and top mantissa bit
+// (as K4 computes it) in 2^(VCT_SPEC_TAU_BITS - 3) classes per octave (quarter octaves by
+// default), from its exponent and top mantissa bits
 __device__ __forceinline__ uint32_t tau_class(float rough) {
     const float tau = fminf(fmaxf(rough, VCT_SPEC_TAU_MIN), VCT_SPEC_TAU_MAX);
     const int ex = (int)((__float_as_uint(tau) >> 23) & 0xffu) - 127;   // -6 .. 0
@@ -207,7 +208,8 @@ __global__ void __launch_bounds__(256) k_scan_reduce(const uint32_t* __restrict_
     if (threadIdx.x == 0) tiles[blockIdx.x] = total;
 }
 
-// exclusive scan of the tile sums in one block (ntiles <= 2^21 / 4096 + 1 = 513: three rounds)
+// exclusive scan of the tile sums in one block (counters <= 2^22 + 1, so ntiles <= 2^22 / 4096
+// + 1 = 1025: five rounds of 256)
 __global__ void __launch_bounds__(256) k_scan_tiles(uint32_t* __restrict__ tiles, uint32_t ntiles) {
     uint32_t carry = 0;
     for (uint32_t b = 0; b < ntiles; b += 256) {

@@ -1820,8 +1820,9 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
     if (!c->n_cu && hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
         c->n_cu = 0;
     const bool lpt_size = c->n_cu > 0 && blocks <= (uint32_t)c->n_cu * 4u * kOccWaves * kLptMaxGenerations;
+    const uint32_t per_class = (blocks + 7u) / 8u;   // units of residue class 0, the largest
     if (deflt && !cnt_form && !(a->variant & kVarNoLpt) && c->k4tune.cur >= 0 && !c->k4_dbg_order && !c->k4_dbg_dur &&
-        blocks / 8u <= kLptMaxPerClass && !c->k4tune.multi && (lpt_size || (a->variant & kVarLptAll))) {
+        per_class <= kLptMaxPerClass && !c->k4tune.multi && (lpt_size || (a->variant & kVarLptAll))) {
         K4Tuner::Entry& te = c->k4tune.e[c->k4tune.cur];
         if (te.chosen >= 0) {
             if (te.hist_cap < blocks) {
@@ -1844,13 +1845,14 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
                 void* op = nullptr;
                 hipError_t e = k4_scratch(c, kScOrder, (size_t)blocks * sizeof(uint32_t), &op, nullptr);
                 if (e != hipSuccess) return e;
-                if ((a->variant & kVarLptSort) || blocks / 8u > (uint32_t)kLptRounds * 1024u)
-                    hipLaunchKernelGGL(k4_lpt_order, dim3(8), dim3(1024), (blocks + 7u) / 8u, c->stream,
+                if ((a->variant & kVarLptSort) || per_class > (uint32_t)kLptRounds * 1024u)
+                    hipLaunchKernelGGL(k4_lpt_order, dim3(8), dim3(1024), per_class, c->stream,
                                        (const uint32_t*)te.hist, blocks, (uint32_t*)op);
                 else
                     hipLaunchKernelGGL(k4_lpt_bands, dim3(8), dim3(1024), 0, c->stream, (const uint32_t*)te.hist,
                                        blocks, (uint32_t*)op);
                 k.order = (const uint32_t*)op;
+                ++c->k4_lpt_launches;
             }
             k.dur = te.hist;
             te.hist_units = blocks;
@@ -1901,6 +1903,9 @@ extern "C" int vct_debug_k4_sched(vct_ctx* c, const uint32_t* order, uint32_t* d
     c->k4_dbg_dur = dur;
     return 0;
 }
+
+// Test hook: the number of K4 launches of this context dispatched in a longest-first order.
+extern "C" long long vct_debug_k4_lpt_launches(const vct_ctx* c) { return c ? (long long)c->k4_lpt_launches : -1; }
 
 #if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
 extern "C" int vct_debug_waves(unsigned long long* out, int n) {   // out[n][3]; n <= 1 << 18

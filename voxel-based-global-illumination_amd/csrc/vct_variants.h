@@ -16,8 +16,9 @@
 //   0x4000     the counting form without counters
 //   bits 16-19 XCD map: 0 default, 1 contiguous runs, 2..6 chunks of 1/4/16/64/256 units
 //   bits 20-23 diffuse parts of the three-part split (2 default)
-//   0x10000000 longest-first dispatch for every settled launch (default: launches of at
-//              most four generations of waves that do not overlap another frame)
+//   0x10000000 longest-first dispatch for settled launches of any size (default: launches
+//              of at most four generations of waves); never for launches that overlap
+//              another frame on a second stream (the order scratch is shared by the streams)
 //   0x20000000 no longest-first dispatch (units in blockIdx order)
 //   0x40000000 ray reordering: one order for every cone part (no specular order)
 //   0x80000000 longest-first dispatch as a full bucket sort (default: four stable bands)

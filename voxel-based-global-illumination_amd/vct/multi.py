@@ -214,6 +214,20 @@ class FrameTracer:
                               steps_px=steps_px, cone_steps=cone_steps, texel_fetches=texel_fetches,
                               tile_rank=self.rank, tile_world=self.world, tile_compact=True, variant=variant)
 
+    def local_planes(self, buf=0):
+        """(diffuse, spec) as trace_local(buf=buf) writes them: the frame (one rank) or this
+        rank's compact tiles; None for a rank without tiles."""
+        if self.world == 1:
+            return self.outs[buf]
+        if self.my_tiles == 0:
+            return None
+        return self.comp[buf][0], self.comp[buf][1]
+
+    @property
+    def last_buf(self):
+        """The buffer set of the latest frame traced by step() / frame()."""
+        return (self.cur - 1) % self.nsets if self._pipelined() else 0
+
     def _nccl(self):
         return self.world > 1 and self.dist.get_backend() == "nccl"
 
