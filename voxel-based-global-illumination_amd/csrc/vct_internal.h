@@ -172,7 +172,8 @@ struct K4Tuner {
     // concurrent frames: once timed launches have come on two streams, each one records
     // `prev_end`, and a timing launch first waits for it (samples stay isolated)
     static constexpr uint64_t kMultiLaunches = 64;   // a stream switch counts for this many launches
-    hipStream_t prev_stream = nullptr;
+    hipStream_t prev_stream = nullptr;        // the last timed launch's stream (the null stream is one too)
+    bool prev_set = false;                    // prev_stream holds a launch's stream
     hipEvent_t prev_end = nullptr;
     uint64_t multi_until = 0;                 // clock value up to which launches count as overlapped
     bool multi = false;                       // clock < multi_until at the last launch

@@ -1572,8 +1572,9 @@ static int k4_form(vct_ctx* c, uint64_t key, const int* cands_in, int n_in, bool
     }
     bool overlapped = false;                     // the previous launch (another stream) still runs
     if (timed) {
-        if (T.prev_stream && T.prev_stream != c->stream) T.multi_until = T.clock + K4Tuner::kMultiLaunches;
+        if (T.prev_set && T.prev_stream != c->stream) T.multi_until = T.clock + K4Tuner::kMultiLaunches;
         T.prev_stream = c->stream;
+        T.prev_set = true;
         T.multi = T.clock < T.multi_until;
         if (T.multi && T.prev_end) overlapped = hipEventQuery(T.prev_end) == hipErrorNotReady;
     }
