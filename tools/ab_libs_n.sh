@@ -16,7 +16,7 @@ for sc in ${SCENES:-atrium courtyard}; do
   for r in $(seq 1 ${ROUNDS:-2}); do
     for lib in $LIBS; do
       VCT_LIB=$L/$lib timeout -k 10 200 python tools/ab.py --variants 0 --rounds 5 --scene $sc ${AB_ARGS:-} > gpurun_out/ab_$lib.json 2>&1 || { tail -5 gpurun_out/ab_$lib.json; exit 1; }
-      echo "$sc $lib $(grep -m1 median gpurun_out/ab_$lib.json) $(grep -o '"steps": [0-9]*' gpurun_out/ab_$lib.json)"
+      echo "$sc $lib $(python3 tools/ab_summary.py gpurun_out/ab_$lib.json)"
     done
   done
 done

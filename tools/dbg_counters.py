@@ -37,7 +37,7 @@ def main():
     lib = _lib.load()
     lib.vct_debug_counters.restype = C.c_int
     lib.vct_debug_counters.argtypes = [C.c_void_p, C.c_int]
-    ctr = (C.c_ulonglong * 48)()
+    ctr = (C.c_ulonglong * 56)()
     g0, E = scenes.grid_for_unit_box(a.n)
     ctx = Context(a.n, g0, E, n_diffuse=a.nd, specular=bool(a.spec))
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -69,7 +69,11 @@ def main():
         if not a.clk:
             print(f"  level B: hit {c[26]} / staged {c[27]} / gather {c[28]} / not sampled {c[31]}; "
                   f"faces-mode brick samples A {c[29]} / B {c[30]}")
-            print(f"  empty-space maps: level-A misses skipped {c[40]}; cluster covers: level A {c[41]} / level B {c[42]}")
+            print(f"  empty-space maps: level-A misses skipped {c[40]}")
+            print(f"  level-B stagings: combined-face march {c[41]} / faces {c[42]} / iso {c[50]}; "
+                  f"while level A hit the cache {c[43]}")
+            print(f"  iso / combined-face gathers {c[53]}: would fit 5^3 {c[51]} / 6^3 {c[52]} / 8x8x3 {c[54]} / "
+                  f"a box of <= 216 texels {c[55]}")
         print(f"  wave-steps: table {c[44]} / per-lane {c[46]}; active lanes {c[45]} "
               f"({c[45] / max(c[44] + c[46], 1):.1f} per wave-step), valid-pixel lanes {c[47] / max(c[44] + c[46], 1):.1f}")
         print(f"  gather reasons: faces not uniform {c[16]}; footprint span (level 0) <=3/<=5/<=9/more {c[18:22]}"

@@ -42,7 +42,7 @@
 // Debug-build counters (make dbg -> vct/libvct_hip_dbg.so, tools/dbg_counters.py):
 // per wave and level sample, which path served it.  Compiled out of the product.
 #if defined(VCT_DEBUG_COUNTERS) || defined(VCT_DEBUG_CLOCK)
-__device__ unsigned long long vct_dbg_ctr[40];
+__device__ unsigned long long vct_dbg_ctr[48];
 __device__ unsigned long long vct_dbg_time[8];
 #endif
 #if defined(VCT_DEBUG_CLOCK) || defined(VCT_DEBUG_WAVES)
@@ -740,7 +740,8 @@ __device__ __forceinline__ float4 brick_sample(const Corner& c, int off, bool on
 
 // debug counters 16..: why a level sample fell back to gathers (too many
 // faces; else the footprint span max-min over the active lanes)
-__device__ __forceinline__ void dbg_fallback_reason(const Corner& c, bool active, bool faces_ok, int l) {
+__device__ __forceinline__ void dbg_fallback_reason(const Corner& c, bool active, bool faces_ok, int l,
+                                                    bool one_slot = false) {
 #ifdef VCT_DEBUG_COUNTERS
     if (!faces_ok) { VCT_DBG(16); return; }
     const int sx = -__ockl_wfred_min_i32(active ? -c.ix : INT_MIN + 1) - __ockl_wfred_min_i32(active ? c.ix : INT_MAX);
@@ -749,6 +750,14 @@ __device__ __forceinline__ void dbg_fallback_reason(const Corner& c, bool active
     const int sp = max(sx, max(sy, sz));
     const int bin = sp <= 3 ? 0 : (sp <= 5 ? 1 : (sp <= 9 ? 2 : 3));
     VCT_DBG((l == 0 ? 18 : 22) + bin);
+    if (one_slot) {             // iso / combined-face gathers: which larger brick would hold them
+        VCT_DBG(45);
+        if (sp <= 3) VCT_DBG(43);                               // 5^3
+        if (sp <= 4) VCT_DBG(44);                               // 6^3
+        const int mn = min(sx, min(sy, sz)), md = sx + sy + sz - sp - mn;
+        if (sp <= 6 && md <= 6 && mn <= 1) VCT_DBG(46);         // 8 x 8 x 3 in some orientation
+        if ((sp + 2) * (md + 2) * (mn + 2) <= 216) VCT_DBG(47); // a box of <= 216 texels
+    }
 #endif
 }
 
@@ -836,6 +845,8 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     }
     Tex4 tB;
     if (stB) tB = stage_load<O32, AM>(k, l1, bB, modeB, cc);
+    if (stB) VCT_DBG(AM == kComb ? 33 : (modeB == kFaces ? 34 : 42));   // level-B stagings by mode
+    if (stB && useA) VCT_DBG(35);                                       // ... while level A hit the cache
     const unsigned long long nzA = useA ? amA : wballot(zbit(k, l0, cA) != 0u) & amA;
     const bool emptyA = nzA == 0ull;                  // the sample is exactly +0
     if (!useA && emptyA) VCT_DBG(32);
@@ -889,13 +900,13 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // others' sample is exactly +0 already)
     if (!useA && !emptyA) {
         VCT_DBG(4 + (l0 < 10 ? l0 : 10));
-        dbg_fallback_reason(cA, active, modeA != kFaces || faces_okA, l0);
+        dbg_fallback_reason(cA, active, modeA != kFaces || faces_okA, l0, AM == kComb || modeA != kFaces);
         if (__builtin_amdgcn_inverse_ballot_w64(nzA))
             sA = sample_level<O32, true, gather_chunk<UNION>()>(k, l0, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(), ld.wy(), ld.wz());
     }
     if (needB && !useB) {
         VCT_DBG(4 + (l1 < 10 ? l1 : 10));
-        dbg_fallback_reason(cB, activeB, modeB != kFaces || faces_okB, l1);
+        dbg_fallback_reason(cB, activeB, modeB != kFaces || faces_okB, l1, AM == kComb || modeB != kFaces);
         if (activeB)
             sB = sample_level<O32, true, gather_chunk<UNION>()>(k, l1, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(), ld.wy(), ld.wz());
     }
@@ -1915,15 +1926,15 @@ extern "C" int vct_debug_waves(unsigned long long* out, int n) {   // out[n][3];
 }
 #endif
 #if defined(VCT_DEBUG_COUNTERS) || defined(VCT_DEBUG_CLOCK)
-extern "C" int vct_debug_counters(unsigned long long* out, int reset) {   // out[48]: 32 counters, 8 clocks, 8 more counters
+extern "C" int vct_debug_counters(unsigned long long* out, int reset) {   // out[56]: 32 counters, 8 clocks, 16 more counters
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out + 40, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 8,
+    if (hipMemcpyFromSymbol(out + 40, HIP_SYMBOL(vct_dbg_ctr), sizeof(unsigned long long) * 16,
                             sizeof(unsigned long long) * 32) != hipSuccess)
         return -1;
     if (hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(vct_dbg_time), sizeof(unsigned long long) * 8) != hipSuccess)
         return -1;
     if (reset) {
-        unsigned long long z[40] = {};
+        unsigned long long z[48] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(vct_dbg_ctr), z, sizeof z) != hipSuccess) return -1;
         if (hipMemcpyToSymbol(HIP_SYMBOL(vct_dbg_time), z, sizeof(unsigned long long) * 8) != hipSuccess) return -1;
     }
