@@ -816,7 +816,7 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const Corner cA = level_corner(l0, qx, qy, qz);
     BrickEntry bA = bc.a;
     bool useA = bA.lvl == l0 && wall_in(amA, in_brick(cA, bA, z3A));
-    Corner cB = cA;
+    Corner cB;                                 // read only where needB (no copies of cA per step)
     BrickEntry bB = bc.b;
     bool useB = false;
     if (needB) {
@@ -880,21 +880,24 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     }
     if (stA || stB) wave_lds_sync();
     pc.mark(2);
-    float4 sA = z4, sB = z4;
     const bool readA = useA && !bA.zero, readB = useB && !bB.zero;
     if (useA) VCT_DBG(bA.zero ? 17 : 15);          // level-A samples from zero / nonzero bricks
-    if (readA || readB) {
-        // every lane samples (no exec-mask branches): an inactive lane reads the brick's
-        // corner-0 texels instead of its own (staged, finite), and its march adds nothing
-        // (march_brick scales the sample by 0)
-        if (readA)
-            sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA) : 0, AM == kComb || modeA != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr), ld.bz(cc.bstr),
-                                  ld.wx(), ld.wy(), ld.wz(), ldsA);
-        if (readB)
-            sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB) : 0, AM == kComb || modeB != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr),
-                                  ld.bz(cc.bstr), ld.wx(), ld.wy(), ld.wz(), ldsB);
-        wave_lds_sync();
-    }
+    // every lane samples (no exec-mask branches): an inactive lane reads the brick's
+    // corner-0 texels instead of its own (staged, finite), and its march adds nothing
+    // (march_brick scales the sample by 0).  The +0 of an unread level is assigned on its
+    // own branch (an initial value would be materialised on every path of the step)
+    float4 sA, sB;
+    if (readA)
+        sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA) : 0, AM == kComb || modeA != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr), ld.bz(cc.bstr),
+                              ld.wx(), ld.wy(), ld.wz(), ldsA);
+    else
+        sA = z4;
+    if (readB)
+        sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB) : 0, AM == kComb || modeB != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr),
+                              ld.bz(cc.bstr), ld.wx(), ld.wy(), ld.wz(), ldsB);
+    else
+        sB = z4;
+    if (readA || readB) wave_lds_sync();
     pc.mark(3);
     // per-lane gathers (level A: only the lanes whose footprint may be nonzero load; the
     // others' sample is exactly +0 already)
