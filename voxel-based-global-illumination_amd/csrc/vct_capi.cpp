@@ -340,6 +340,7 @@ void vct_destroy(vct_ctx* c) {
                     if (e) (void)hipEventDestroy(e);
         if (en.hist) (void)hipFree(en.hist);
     }
+    for (uint32_t* h : c->k4tune.retired) (void)hipFree(h);
     if (c->k4tune.prev_end) (void)hipEventDestroy(c->k4tune.prev_end);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

@@ -175,6 +175,9 @@ struct K4Tuner {
     hipStream_t prev_stream = nullptr;        // the last timed launch's stream (the null stream is one too)
     bool prev_set = false;                    // prev_stream holds a launch's stream
     hipEvent_t prev_end = nullptr;
+    // duration buffers outgrown by a larger workload: a launch on another stream may still
+    // write them, so they are freed with the context, not in the launch path
+    std::vector<uint32_t*> retired;
     uint64_t multi_until = 0;                 // clock value up to which launches count as overlapped
     bool multi = false;                       // clock < multi_until at the last launch
 };

@@ -1843,16 +1843,18 @@ hipError_t launch_trace(vct_ctx* c, const vct_trace_args* a) {
             if (te.hist_cap < blocks) {
                 if (te.hist) {
                     // a launch on any stream may still write it (the durations are shared by the
-                    // streams; only an entry taken over by a larger workload gets here)
-                    hipError_t e = hipDeviceSynchronize();
-                    if (e != hipSuccess) return e;
-                    (void)hipFree(te.hist);
+                    // streams; only an entry taken over by a larger workload gets here): retired,
+                    // freed with the context -- no device-wide wait in the launch path
+                    c->k4tune.retired.push_back(te.hist);
                     te.hist = nullptr;
                     te.hist_cap = 0;
                 }
-                hipError_t e = hipMalloc((void**)&te.hist, (size_t)blocks * sizeof(uint32_t));
+                // the first buffer covers every launch the default rule dispatches longest first
+                const uint32_t cap = blocks > (uint32_t)c->n_cu * 4u * kOccWaves * kLptMaxGenerations
+                                         ? blocks : (uint32_t)c->n_cu * 4u * kOccWaves * kLptMaxGenerations;
+                hipError_t e = hipMalloc((void**)&te.hist, (size_t)cap * sizeof(uint32_t));
                 if (e != hipSuccess) return e;
-                te.hist_cap = blocks;
+                te.hist_cap = cap;
                 te.hist_ok = false;
             }
             if (te.hist_units != blocks || te.hist_cand != cand) te.hist_ok = false;
