@@ -239,6 +239,12 @@ def roofline(rec, reason, k4_ms, texels, valid_px, profile_path, key, steps=None
         # wave instructions per cone step (a wave-step advances ~62 lanes' cone steps)
         out["valu_per_cone_step"] = round(valu / steps, 3)
         out["salu_per_cone_step"] = round(salu / steps, 3)
+    if rec.get("effective_clock_ghz"):
+        # the chip runs below the 2.4 GHz the peak assumes (DVFS under load); the VALU
+        # fraction against the issue rate at the clock measured on the profiled dispatches
+        ghz = rec["effective_clock_ghz"]
+        out["effective_clock_ghz"] = round(ghz, 3)
+        out["valu_frac_at_measured_clock"] = round(v_ach / (1024 * ghz / 2), 4)
     if rec.get("SQ_WAVE_CYCLES"):
         # fraction of wave cycles in which the wave issued (the rest: waits and issue stalls)
         out["issue_active"] = round(rec["SQ_ACTIVE_INST_ANY"] / rec["SQ_WAVE_CYCLES"], 4)

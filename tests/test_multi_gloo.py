@@ -176,9 +176,17 @@ def _tracer_worker(rank, world, port, out_dir, mode, w, h):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     tr = FrameTracer(PatternContext(torch), torch, dist, w, h, rank, world, torch.device("cpu"), mode=mode)
+    # bench.py's timed_equals_counting: this rank's planes of the first (counting) frame
+    # against those of the last pipelined frame
+    tr.trace_local((None, None, None), (0.0, 0.0, 3.0), buf=0)
+    lp = tr.local_planes(0)
+    first = None if lp is None else (lp[0].clone(), lp[1].clone())
     for _ in range(3):
         tr.step((None, None, None), (0.0, 0.0, 3.0))
     tr.drain()
+    lp = tr.local_planes(tr.last_buf)
+    assert (lp is None) == (first is None) == (tr.my_tiles == 0)
+    assert first is None or (torch.equal(lp[0], first[0]) and torch.equal(lp[1], first[1]))
     if tr.holds_frame:
         np.save(os.path.join(out_dir, f"t{rank}.npy"), np.concatenate([tr.diff.numpy(), tr.spec.numpy()], -1))
     dist.destroy_process_group()

@@ -94,6 +94,12 @@ def k4_record(passes):
         for c in sorted(names):
             v = [e["ctr"][c] for e in sel if c in e["ctr"]]
             rec[c] = sum(v) / len(v)
+        # effective shader clock of the same dispatches: GRBM_GUI_ACTIVE counts busy cycles
+        # summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back); read high below ~0.3 ms
+        ck = [e["ctr"]["GRBM_GUI_ACTIVE"] / 8.0 / e["dur_ns"] for e in sel
+              if "GRBM_GUI_ACTIVE" in e["ctr"] and e["dur_ns"]]
+        if ck:
+            rec["effective_clock_ghz"] = sum(ck) / len(ck)
     return rec
 
 

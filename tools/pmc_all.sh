@@ -4,7 +4,8 @@
 # rand = `stress`, c4 / c5 = `multi_config`; "wl:N" = rank 0's launch of the N-rank
 # split) two rocprofv3 runs of the same command, each with --kernel-trace and one
 # counter group (the per-block slot limits of MI355X_MICROARCH.md 'rocprofv3 PMC
-# slots': 8 SQ + TCC hit / miss + WRITE_SIZE; FETCH_SIZE + the L2's atomic requests),
+# slots': 8 SQ + TCC hit / miss + WRITE_SIZE; FETCH_SIZE + the L2's atomic requests + the
+# GPU-busy clock count GRBM_GUI_ACTIVE, summed over the 8 XCDs: the effective clock),
 # then tools/make_pmc_records.py writes the records, stamped with the library's sha256.
 #   TAG=r4a WLS="c3 courtyard rand c4 c5 c3:2 c3:4 c3:8" bash tools/pmc_all.sh
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -21,7 +22,7 @@ for spec in $WLS; do
   OUT=$ROOT/${wl}_ranks$N
   mkdir -p $OUT
   for pass in a b; do
-    if [ $pass = a ]; then PMC="$SQ TCC_HIT_sum TCC_MISS_sum WRITE_SIZE"; else PMC="FETCH_SIZE TCC_EA0_ATOMIC_sum"; fi
+    if [ $pass = a ]; then PMC="$SQ TCC_HIT_sum TCC_MISS_sum WRITE_SIZE"; else PMC="FETCH_SIZE TCC_EA0_ATOMIC_sum GRBM_GUI_ACTIVE"; fi
     timeout -s KILL ${PASS_TIMEOUT:-240} rocprofv3 --kernel-trace --pmc $PMC -d $OUT/$pass -o $pass --output-format csv \
         -- python3 tools/pmc_workload.py --wl $wl --world $N --rank 0 > $OUT/$pass.stdout 2> $OUT/$pass.stderr
     rc=$?
