@@ -10,7 +10,7 @@ for r in $(seq 1 ${ROUNDS:-1}); do
     name=${c%%:*}; args=${c#*:}
     for lib in $LIBS; do
       VCT_LIB=$L/$lib timeout -k 10 300 python tools/ab.py --variants ${VARIANT:-0} --rounds 3 --reps 3 $args > gpurun_out/abc_$lib.json 2>&1 || { tail -5 gpurun_out/abc_$lib.json; exit 1; }
-      echo "$name $lib $(grep -m1 median gpurun_out/abc_$lib.json) $(grep -o '"steps": [0-9]*' gpurun_out/abc_$lib.json) $(grep -o '"k4_form": [-0-9a-z]*' gpurun_out/abc_$lib.json)"
+      echo "$name $lib $(python3 tools/ab_summary.py gpurun_out/abc_$lib.json) $(grep -o '"k4_form": [-0-9a-z]*' gpurun_out/abc_$lib.json)"
     done
   done
 done
