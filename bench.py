@@ -720,13 +720,17 @@ def measure_scene(args, torch, dist, ctx, scene_name, rank, world, dev, stream, 
     timed_equals_counting = max_over_ranks(torch, dist, dev, [0.0 if same else 1.0], world)[0] == 0.0
     del counted
     k4_ov_ms = [a.elapsed_time(b) for a, b in ev]
-    # K4 alone (the roofline's launch duration): K frames back to back on the ctx stream,
-    # no other work on the GPU -- in the pipelined loop consecutive traces share the chip
+    # K4 alone (the roofline's launch duration): K frames on the ctx stream, each launch by
+    # itself (the end event waited for before the next launch), no other work on the GPU --
+    # in the pipelined loop consecutive traces share the chip.  (Queued back to back, the
+    # event pairs also caught the time between launches: 1-2 % above the rocprofv3
+    # durations of the same kernel; launched one at a time they agree with them.)
     iev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     for s in range(args.steps):
         iev[s][0].record(stream)
         tracer.trace_local(gb, eye, variant=args.variant)
         iev[s][1].record(stream)
+        iev[s][1].synchronize()
     torch.cuda.synchronize()
     k4_ms = [a.elapsed_time(b) for a, b in iev]
     k4_avg_ms = sum(k4_ms) / len(k4_ms)
