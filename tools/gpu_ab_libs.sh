@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-6 K4 A/B lease: path counters of a debug build, then tools/ab_libs_n.sh over $LIBS
+# K4 A/B on one box: path counters of a debug build (DBG_LIB), then tools/ab_libs_n.sh over $LIBS
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
 L=voxel-based-global-illumination_amd/vct
 if [ -n "$DBG_LIB" ]; then
