@@ -783,7 +783,7 @@ def form_name(f):
     """vct_trace_form -> its description (None while timing)"""
     if f is None or f < 0:
         return None
-    return ("occupancy, 5 waves/SIMD" if f & 1 else "union (bricks of up to five faces), 4 waves/SIMD") + (
+    return ("occupancy, 5 waves/SIMD" if f & 1 else "union (bricks of up to six faces), 4 waves/SIMD") + (
         ", ray reordering" if f & 2 else ", screen order")
 
 

@@ -110,7 +110,7 @@ __device__ __forceinline__ float lvl_coord(float q, float scale) {
 // the occupancy form of the default cone trace: 96 VGPRs, 7008 B of LDS (no four-face
 // union), 5 waves/SIMD; the union form runs kUnionWaves (K4Tuner picks per workload)
 constexpr int kOccWaves = 5;   // 6 (80 VGPRs) spills 54-69 VGPRs
-constexpr int kUnionWaves = 4;  // __launch_bounds__ minimum waves per SIMD (128 VGPRs, 9344 B of LDS)
+constexpr int kUnionWaves = 4;  // __launch_bounds__ minimum waves per SIMD (128 VGPRs, 9984 B of LDS)
 
 namespace vct {
 namespace {
@@ -219,6 +219,10 @@ constexpr int kChOcc = VCT_K4_CHOCC;
 // the union form stages five-face cones too (4 x 4 x 3 bricks)
 #ifndef VCT_K4_FIVE
 #define VCT_K4_FIVE 1
+#endif
+// ... and six-face cones (4 x 4 x 3 bricks in the kBz6 layout, a march of their own)
+#ifndef VCT_K4_SIX
+#define VCT_K4_SIX 1
 #endif
 template <bool UNION> constexpr int gather_chunk() { return UNION ? kCh : kChOcc; }
 
@@ -488,13 +492,23 @@ __device__ __forceinline__ uint32_t march(const TraceK& k, float ox, float oy, f
 // every z step onto the same banks.
 constexpr int kBz = 19;
 constexpr int kBlk = 3 * kBz + 16;              // one face block: 73 slots
-// four-face cones in the occupancy form: 4 x 4 x 3 bricks, four 54-slot face blocks
-// (216 slots) in the 219-slot entry
-constexpr int kBlk3 = 2 * kBz + 16;
-// float4 slots per cache entry: up to 4 face blocks (3 without the four-face union)
-// The two cache entries live in LDS regions 0 and 1 (entry a in region `flip`): 9344 B
-// per wave with the union (4 waves/SIMD fit the 160 KB), 7008 B without (5 waves/SIMD).
-template <bool UNION> constexpr int entry_slots() { return (UNION ? 4 : 3) * kBlk; }
+// 4 x 4 x 3 bricks: a face block of 2 BZ + 16 slots.  Four-face cones in the occupancy
+// form: four 54-slot blocks (216 slots) in the 219-slot entry.  Six-face cones in the
+// union form: six blocks in the BZ = kBz6 layout (6 x 52 = 312 slots; six 54-slot blocks,
+// 324, would not let 16 waves' two entries fit the 160 KB).  18 = 2 mod 16 keeps the
+// x / y spans distinct mod 16 and costs a two-way conflict where a 16-lane group spans
+// three corners in x and two in z.
+template <int BZ> constexpr int blk3() { return 2 * BZ + 16; }
+constexpr int kBlk3 = blk3<kBz>();
+constexpr int kBz6 = 18;
+constexpr int kBlk6 = blk3<kBz6>();
+// float4 slots per cache entry: up to 4 face blocks (3 without the four-face union), or
+// six 4 x 4 x 3 blocks.  The two cache entries live in LDS regions 0 and 1 (entry a in
+// region `flip`): 9984 B per wave with the six-face union (4 waves/SIMD fit the 160 KB),
+// 7008 B without the union (5 waves/SIMD).
+template <bool UNION> constexpr int entry_slots() {
+    return UNION ? (VCT_K4_SIX && 6 * kBlk6 > 4 * kBlk ? 6 * kBlk6 : 4 * kBlk) : 3 * kBlk;
+}
 template <bool UNION> constexpr int lds_slots() { return 2 * entry_slots<UNION>(); }
 
 // One wave's LDS hand-off (writes -> other lanes' reads, and reads -> next
@@ -508,13 +522,13 @@ __device__ __forceinline__ void wave_lds_sync() {
 struct ConeCtl {                 // wave-uniform facts about one cone
     int funion;                  // faces (bit per VCT_FACE_*) any valid lane selects
     int nfaces;                  // popcount(funion)
-    int f0, f1, f2, f3, f4;      // the faces of funion in increasing order (first nfaces valid)
+    int f0, f1, f2, f3, f4, f5;  // the faces of funion in increasing order (first nfaces valid)
     bool dir_uniform;            // every valid lane has the same wd = d^2 (bitwise) and the same faces
     int neg;                     // bit a: every valid lane moves toward -axis a (brick slack goes there)
     float uwx, uwy, uwz;         // that wd
     int z3;                      // 1: faces-mode bricks are 4 x 4 x 3 (a four-face cone in the occupancy form,
-                                 // a five-face cone in the union form)
-    int bstr;                    // faces-mode block stride (kBlk, or kBlk3 with z3)
+                                 // a five- or six-face cone in the union form)
+    int bstr;                    // faces-mode block stride (kBlk, kBlk3 with z3, kBlk6 for six faces)
 };
 
 struct BrickEntry {
@@ -643,10 +657,11 @@ __device__ __forceinline__ uint32_t bits4(float4 v) {
 }
 
 // stores this lane's staging texel(s); returns true when every value it stored is +0
-template <int AM = -1>
+template <int AM = -1, int BZ = kBz>
 __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const Tex4& t, float4* __restrict__ lds) {
+    constexpr int B3 = blk3<BZ>();
     const int lane = lane_id_opaque();
-    float4* p = lds + ((lane & 15) + kBz * (lane >> 4));
+    float4* p = lds + ((lane & 15) + BZ * (lane >> 4));
     uint32_t nz;
     if (mode == kIso) {
         p[0] = t.a;
@@ -659,9 +674,9 @@ __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const T
         nz = 0u;
         if (lane < 48) {
             p[0] = t.a;
-            p[kBlk3] = t.b;
-            p[2 * kBlk3] = t.c;
-            p[3 * kBlk3] = t.d;
+            p[B3] = t.b;
+            p[2 * B3] = t.c;
+            p[3 * B3] = t.d;
             nz = bits4(t.a) | bits4(t.b) | bits4(t.c) | bits4(t.d);
         }
     } else {
@@ -677,12 +692,12 @@ __device__ __forceinline__ bool stage_store(int mode, const ConeCtl& cc, const T
     return nz == 0u;
 }
 
-// the fifth face block of a five-face brick (union form, 4 x 4 x 3): face f4 at block 4,
-// staged after the other four (its texel is not held with them: the union form has no
-// VGPRs to spare); true when the lane stored +0 only
-template <bool O32>
-__device__ __forceinline__ bool stage_face5(const TraceK& k, int l, const BrickEntry& be, const ConeCtl& cc,
-                                            float4* __restrict__ lds) {
+// the fifth (sixth) face block of a five- (six-) face brick (union form, 4 x 4 x 3): face
+// `face` at block `blk`, staged after the other four (its texel is not held with them: the
+// union form has no VGPRs to spare); true when the lane stored +0 only
+template <bool O32, int BZ = kBz>
+__device__ __forceinline__ bool stage_face(const TraceK& k, int l, const BrickEntry& be, int face, int blk,
+                                           float4* __restrict__ lds) {
     const int nl = k.n >> l;
     const int lane = lane_id_opaque();
     const int sx = be.ox + (lane & 3), sy = be.oy + ((lane >> 2) & 3), sz = be.oz + (lane >> 4);
@@ -690,23 +705,24 @@ __device__ __forceinline__ bool stage_face5(const TraceK& k, int l, const BrickE
     const uint32_t gi = texel_index_lg((uint32_t)sx, (uint32_t)sy, (uint32_t)sz, (uint32_t)(k.lgn - l));
     const LevelView<O32> lv = level_view<O32>(k, l);
     const uint32_t sh = 3u * (uint32_t)(k.lgn - l);
-    const float4 v = lv.fetch(((uint32_t)cc.f4 << sh) + gi, inb);
+    const float4 v = lv.fetch(((uint32_t)face << sh) + gi, inb);
     uint32_t nz = 0u;
     if (lane < 48) {
-        lds[(lane & 15) + kBz * (lane >> 4) + 4 * kBlk3] = v;
+        lds[(lane & 15) + BZ * (lane >> 4) + blk * blk3<BZ>()] = v;
         nz = bits4(v);
     }
     return nz == 0u;
 }
 
 // slot of the lane's corner 0 in a staged entry
+template <int BZ = kBz>
 __device__ __forceinline__ int brick_slot(const Corner& c, const BrickEntry& be) {
-    return (c.ix - be.ox) + 4 * (c.iy - be.oy) + __mul24(kBz, c.iz - be.oz);
+    return (c.ix - be.ox) + 4 * (c.iy - be.oy) + __mul24(BZ, c.iz - be.oz);
 }
 
 // D_l from a staged brick: corner 0 at slot `off`; faces mode reads the lane's own
 // face blocks at float4 offsets bx, by, bz
-template <int KL>   // corners x 3 faces per LDS burst in faces mode
+template <int KL, int BZ = kBz>   // KL: corners x 3 faces per LDS burst in faces mode
 __device__ __forceinline__ float4 brick_sample(const Corner& c, int off, bool one_slot, int bx,
                                                int by, int bz, float wdx, float wdy, float wdz,
                                                const float4* __restrict__ lds) {
@@ -717,7 +733,7 @@ __device__ __forceinline__ float4 brick_sample(const Corner& c, int off, bool on
     if (one_slot) {
         float4 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = b[(i & 1) + 4 * ((i >> 1) & 1) + kBz * (i >> 2)];
+        for (int i = 0; i < 8; ++i) v[i] = b[(i & 1) + 4 * ((i >> 1) & 1) + BZ * (i >> 2)];
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc_fma(acc, wc[i], v[i]);
     } else {
@@ -727,7 +743,7 @@ __device__ __forceinline__ float4 brick_sample(const Corner& c, int off, bool on
             float4 vx[KL], vy[KL], vz[KL];
 #pragma unroll
             for (int i = 0; i < KL; ++i) {
-                const int o = ((h + i) & 1) + 4 * (((h + i) >> 1) & 1) + kBz * ((h + i) >> 2);
+                const int o = ((h + i) & 1) + 4 * (((h + i) >> 1) & 1) + BZ * ((h + i) >> 2);
                 vx[i] = X[o]; vy[i] = Y[o]; vz[i] = Z[o];
             }
 #pragma unroll
@@ -784,8 +800,9 @@ struct LaneDir {
 // Each level is served from the cache, restaged (both levels' loads in one
 // batch) or, when the wave's footprint does not fit, gathered per lane.
 // AM: the cone's anisotropic staging mode when march_brick specialised the march on it
-// (kComb for dir_uniform cones, kFaces otherwise; -1 = read cc.dir_uniform per step)
-template <bool O32, bool UNION, int KL, int AM = -1>
+// (kComb for dir_uniform cones, kFaces otherwise; -1 = read cc.dir_uniform per step).
+// BZ = kBz6: the march of a six-face cone (union form), every brick in that layout.
+template <bool O32, bool UNION, int KL, int AM = -1, int BZ = kBz>
 __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx, float qy, float qz,
                                               unsigned long long amA, unsigned long long amB, float fr, const ConeCtl& cc, const LaneDir& ld,
                                               float4* __restrict__ lds, BrickCache& bc, PhaseClock& pc) {
@@ -798,7 +815,8 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     const int aniso_mode = AM >= 0 ? AM : (cc.dir_uniform ? kComb : kFaces);
     const int modeA = (l0 == 0 || !k.aniso) ? kIso : aniso_mode;
     const int modeB = k.aniso ? aniso_mode : kIso;
-    const bool faces_ok = AM == kComb || cc.nfaces <= (UNION && VCT_K4_FIVE ? 5 : 4);
+    constexpr int kMaxFaces = UNION && VCT_K4_FIVE ? (VCT_K4_SIX && BZ == kBz6 ? 6 : 5) : 4;
+    const bool faces_ok = AM == kComb || cc.nfaces <= kMaxFaces;
     // faces-mode levels of a four-face cone in the occupancy form: 4 x 4 x 3 bricks
     // (a dir_uniform cone has three faces: never z3)
     const int z3A = AM != kComb && modeA == kFaces ? cc.z3 : 0, z3B = AM != kComb && modeB == kFaces ? cc.z3 : 0;
@@ -854,8 +872,9 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // zero (fmaf(w, +0, +0) = +0 through the whole trilinear chain), so hits on it skip
     // the LDS reads and the FMAs
     if (stB) {
-        bool zB = stage_store<AM>(modeB, cc, tB, ldsB);
-        if (UNION && VCT_K4_FIVE && AM != kComb && modeB == kFaces && cc.nfaces > 4) zB = stage_face5<O32>(k, l1, bB, cc, ldsB) && zB;
+        bool zB = stage_store<AM, BZ>(modeB, cc, tB, ldsB);
+        if (UNION && VCT_K4_FIVE && AM != kComb && modeB == kFaces && cc.nfaces > 4) zB = stage_face<O32, BZ>(k, l1, bB, cc.f4, 4, ldsB) && zB;
+        if (kMaxFaces > 5 && modeB == kFaces) zB = stage_face<O32, BZ>(k, l1, bB, cc.f5, 5, ldsB) && zB;
         bB.zero = bc.b.zero = wall(zB);
     }
     bool stA = false;
@@ -874,8 +893,9 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     if (useB && modeB == kFaces) VCT_DBG(30);
     pc.mark(1);
     if (stA) {
-        bool zA = stage_store<AM>(modeA, cc, stage_load<O32, AM>(k, l0, bA, modeA, cc), ldsA);
-        if (UNION && VCT_K4_FIVE && AM != kComb && modeA == kFaces && cc.nfaces > 4) zA = stage_face5<O32>(k, l0, bA, cc, ldsA) && zA;
+        bool zA = stage_store<AM, BZ>(modeA, cc, stage_load<O32, AM>(k, l0, bA, modeA, cc), ldsA);
+        if (UNION && VCT_K4_FIVE && AM != kComb && modeA == kFaces && cc.nfaces > 4) zA = stage_face<O32, BZ>(k, l0, bA, cc.f4, 4, ldsA) && zA;
+        if (kMaxFaces > 5 && modeA == kFaces) zA = stage_face<O32, BZ>(k, l0, bA, cc.f5, 5, ldsA) && zA;
         bA.zero = bc.a.zero = wall(zA);
     }
     if (stA || stB) wave_lds_sync();
@@ -888,12 +908,12 @@ __device__ __forceinline__ float4 step_bricks(const TraceK& k, int l0, float qx,
     // own branch (an initial value would be materialised on every path of the step)
     float4 sA, sB;
     if (readA)
-        sA = brick_sample<KL>(cA, active ? brick_slot(cA, bA) : 0, AM == kComb || modeA != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr), ld.bz(cc.bstr),
+        sA = brick_sample<KL, BZ>(cA, active ? brick_slot<BZ>(cA, bA) : 0, AM == kComb || modeA != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr), ld.bz(cc.bstr),
                               ld.wx(), ld.wy(), ld.wz(), ldsA);
     else
         sA = z4;
     if (readB)
-        sB = brick_sample<KL>(cB, activeB ? brick_slot(cB, bB) : 0, AM == kComb || modeB != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr),
+        sB = brick_sample<KL, BZ>(cB, activeB ? brick_slot<BZ>(cB, bB) : 0, AM == kComb || modeB != kFaces, ld.bx(cc.bstr), ld.by(cc.bstr),
                               ld.bz(cc.bstr), ld.wx(), ld.wy(), ld.wz(), ldsB);
     else
         sB = z4;
@@ -1020,6 +1040,8 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.f3 = __builtin_ctz(u | 64);
         u &= u - 1;
         cc.f4 = __builtin_ctz(u | 64);
+        u &= u - 1;
+        cc.f5 = __builtin_ctz(u | 64);
         // a background lane's faces may lie outside the union (which only the valid lanes
         // define): it gets block 0, so its (discarded) brick samples read staged texels
         ld.blk = valid ? (uint32_t)__builtin_popcount(cc.funion & ((1 << fx) - 1)) |
@@ -1031,9 +1053,10 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         cc.uwz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wdz), fl));
         // same d^2 everywhere AND one face per axis (d and -d share d^2)
         cc.dir_uniform = wall_in(vm, (wdx == cc.uwx) & (wdy == cc.uwy) & (wdz == cc.uwz)) && cc.nfaces == 3;
-        // the union form's 292-slot entries hold five 4 x 4 x 3 face blocks (270 slots)
-        cc.z3 = (!UNION && cc.nfaces == 4) || (UNION && VCT_K4_FIVE && cc.nfaces == 5) ? 1 : 0;
-        cc.bstr = cc.z3 ? kBlk3 : kBlk;
+        // the union form's entries hold five 4 x 4 x 3 face blocks (270 slots) or six in
+        // the kBz6 layout (312)
+        cc.z3 = (!UNION && cc.nfaces == 4) || (UNION && VCT_K4_FIVE && cc.nfaces >= 5) ? 1 : 0;
+        cc.bstr = UNION && VCT_K4_SIX && cc.nfaces == 6 ? kBlk6 : (cc.z3 ? kBlk3 : kBlk);
     }
     BrickCache bc;
     bc.a = bc.b = BrickEntry{-1, 0, 0, 0, 0};
@@ -1043,8 +1066,9 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
     // cone stages face blocks, so the per-step mode selects, the four-face / z3 tests
     // and the faces-mode sampling fold away in the combined-face copy.  (Specialising
     // the per-lane specular march too measured slower: -1.0 % instead of -1.6 %.)
-    auto march_loop = [&](auto am_tag) __attribute__((always_inline)) {
+    auto march_loop = [&](auto am_tag, auto bz_tag) __attribute__((always_inline)) {
     constexpr int AM = decltype(am_tag)::value;
+    constexpr int BZ = decltype(bz_tag)::value;
     for (int i = 0;; ++i) {
         asm volatile("" : "+v"(dx), "+v"(dy), "+v"(dz), "+v"(ld.blk));   // see LaneDir
         ld.dx = dx; ld.dy = dy; ld.dz = dz;
@@ -1092,7 +1116,7 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (TAB || wall_in(am, l0 == l0f)) {     // wave-uniform mip pair: brick path
             pc.mark(0);
-            s = step_bricks<O32, UNION, KL, AM>(k, l0f, qx, qy, qz, am, am & two_m, fr, cc, ld, lds, bc, pc);
+            s = step_bricks<O32, UNION, KL, AM, BZ>(k, l0f, qx, qy, qz, am, am & two_m, fr, cc, ld, lds, bc, pc);
         } else if (active) {                    // lanes disagree on the level (per-lane roughness)
             s = sample_level<O32, false, gather_chunk<UNION>()>(k, l0, qx, qy, qz, ld.fx(), ld.fy(), ld.fz(), ld.wx(),
                                                                   ld.wy(), ld.wz());
@@ -1120,9 +1144,11 @@ __device__ __forceinline__ uint32_t march_brick(const TraceK& k, bool valid, flo
         pc.mark(5);
     }
     };
-    if (TAB && cc.dir_uniform) march_loop(std::integral_constant<int, kComb>{});
-    else if (TAB) march_loop(std::integral_constant<int, kFaces>{});
-    else march_loop(std::integral_constant<int, -1>{});
+    using BzStd = std::integral_constant<int, kBz>;
+    if (TAB && cc.dir_uniform) march_loop(std::integral_constant<int, kComb>{}, BzStd{});
+    else if (UNION && VCT_K4_SIX && TAB && cc.nfaces == 6) march_loop(std::integral_constant<int, kFaces>{}, std::integral_constant<int, kBz6>{});
+    else if (TAB) march_loop(std::integral_constant<int, kFaces>{}, BzStd{});
+    else march_loop(std::integral_constant<int, -1>{}, BzStd{});
     res = make_float4(cr, cg, cb, a);
     return steps;
 }

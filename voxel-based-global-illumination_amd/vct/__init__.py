@@ -155,7 +155,7 @@ class Context:
     @property
     def trace_form(self) -> int:
         """Kept candidate of the default cone trace for the current workload (vct_trace_form):
-        bit 0 the form (0 union: bricks of up to five faces, 4 waves/SIMD; 1 occupancy, 5 waves/SIMD), bit 1
+        bit 0 the form (0 union: bricks of up to six faces, 4 waves/SIMD; 1 occupancy, 5 waves/SIMD), bit 1
         ray reordering; -1 while still timing."""
         return int(self.lib.vct_trace_form(self.h))
 
