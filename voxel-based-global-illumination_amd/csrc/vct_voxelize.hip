@@ -22,6 +22,21 @@
 
 #include "vct_internal.h"
 
+#ifdef VCT_DEBUG_WAVES
+// per-wave (start, end, HW_ID | XCC_ID << 32) of the last k2_walk launch (timeline build,
+// tools/k2_waves.py); compiled out of the product
+constexpr int kDbgK2Waves = 1 << 16;
+__device__ unsigned long long vct_dbg_k2_wave[kDbgK2Waves][3];
+extern "C" int vct_debug_k2_waves(unsigned long long* out, int n) {
+    if (n > kDbgK2Waves) n = kDbgK2Waves;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(vct_dbg_k2_wave), sizeof(unsigned long long) * 3 * n) == hipSuccess ? n : -1;
+}
+extern "C" int vct_debug_k2_waves_clear() {
+    static unsigned long long z[kDbgK2Waves][3];
+    return hipMemcpyToSymbol(HIP_SYMBOL(vct_dbg_k2_wave), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
+
 namespace vct {
 namespace {
 
@@ -639,6 +654,9 @@ __global__ void __launch_bounds__(BS) k2_walk(const uint32_t* __restrict__ lit, 
                                                 float ly, float lz, float cr, float cg, float cb,
                                                 float4* __restrict__ r0) {
     __shared__ unsigned long long cbits[kCoarseRows];
+#ifdef VCT_DEBUG_WAVES
+    const unsigned long long wave_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t cnt = *n_lit;
     if (blockIdx.x * BS >= cnt) return;           // block-uniform: no lit voxel for this block
     const int cn = n >> cs;
@@ -660,6 +678,18 @@ __global__ void __launch_bounds__(BS) k2_walk(const uint32_t* __restrict__ lit, 
         r0[l0_texel(v, (uint32_t)n)] =
             make_float4(((ao.x * cr) * ndl) * vis, ((ao.y * cg) * ndl) * vis, ((ao.z * cb) * ndl) * vis, 1.0f);
     }
+#ifdef VCT_DEBUG_WAVES
+    {
+        const uint32_t wid = blockIdx.x * (BS >> 6) + (threadIdx.x >> 6);
+        if ((threadIdx.x & 63) == 0 && wid < (uint32_t)kDbgK2Waves) {
+            vct_dbg_k2_wave[wid][0] = wave_t0;
+            vct_dbg_k2_wave[wid][1] = __builtin_amdgcn_s_memrealtime();
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);      // HW_REG_HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);    // HW_REG_XCC_ID
+            vct_dbg_k2_wave[wid][2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        }
+    }
+#endif
 }
 
 // dense form (one lane per voxel), kept for the voxel-parallel A/B (VCT_K2_DENSE)
